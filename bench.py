@@ -1,0 +1,170 @@
+"""bench.py — sampled molecules/sec for the equivariant-CNF sample path (BASELINE.json `metric`).
+
+Workload (BASELINE.json configs[1]): LJ13 (N = 13, D = 3, lj13.yaml network), batch 1024 molecules per GPU,
+fixed-step ODE with NFE = 100 (Euler, dt = 0.01), fp32, synthetic inputs (x0 from the zero-CoM
+base with a seeded draw) and flax-default random-init weights of the lj13 architecture.
+
+One "step" = one full sample of the batch: x0 (resident in HBM) -> 100 EGNN evaluations -> x1, i.e. one
+ecnf_integrate launch.  Multi-GPU: one process per GPU (torchrun), each rank samples its own 1024 molecules
+(weak scaling, no data-path collective); the timing is the max over ranks.
+
+Extra fields: "roofline" (dominant kernel = integrate_kernel, FP32-MFMA bound: algorithmic FLOPs per launch /
+average launch time from HIP events on the launch stream) and "cpu_baseline" (the oracle's numpy fp32 batched
+restatement of the same Euler solve on a bounded sample, rank 0 at N = 1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "ecnf-baseline-neurips-2023_amd"))
+sys.path.insert(0, ROOT)
+
+PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X dense FP32 matrix peak (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def flops_per_eval(cfg) -> float:
+    """Dense-contraction FLOPs of one EGNN evaluation of one molecule with the phi_e layer-1 per-node
+    factorisation: F = K [2N(H+T)H + 4NHM + 3EM + 2E(L-1)M^2 + 2ELM^2 + 4EM
+    + 2N((M+H)M + (L-1)M^2 + MH)]."""
+    N, H, T, M, L, K = cfg.n_nodes, cfg.hidden, cfg.time_embedding_dim, cfg.mlp_width, cfg.mlp_depth, cfg.n_blocks
+    E = N * (N - 1)
+    return K * (2 * N * (H + T) * H + 4 * N * H * M + 3 * E * M + 2 * E * (L - 1) * M * M + 2 * E * L * M * M
+                + 4 * E * M + 2 * N * ((M + H) * M + (L - 1) * M * M + M * H))
+
+
+def cpu_baseline(cfg_name: str, n_mol: int, nfe: int, threads: int):
+    """Time the oracle (numpy fp32, batched like XLA's vmap) on `n_mol` molecules x `nfe` Euler steps."""
+    import numpy as np
+    from threadpoolctl import threadpool_limits
+    from oracle import ecnf_oracle as O
+    oc = O.CONFIGS[cfg_name]
+    params = O.init_params(oc, 0)
+    rng = np.random.default_rng(0)
+    z = rng.standard_normal((n_mol, oc.n_nodes * oc.dim)).astype(np.float32)
+    x0 = O.base_sample(z, oc)
+    feat = np.zeros((n_mol, oc.n_nodes), np.int32)
+    with threadpool_limits(limits=threads):
+        O.sample_cnf(params, oc, x0[:2], feat[:2], solver="euler", dt0=0.5)   # warm-up
+        t0 = time.perf_counter()
+        O.sample_cnf(params, oc, x0, feat, solver="euler", dt0=1.0 / nfe)
+        dt = time.perf_counter() - t0
+    return n_mol / dt, dt
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=1024, help="molecules per GPU per step")
+    ap.add_argument("--config", default="lj13")
+    ap.add_argument("--nfe", type=int, default=100)
+    ap.add_argument("--cpu-molecules", type=int, default=48, help="bounded CPU-baseline sample (0 = skip)")
+    ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "0") or 0))
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from ecnf_amd import CONFIGS, init_params
+    from ecnf_amd.engine import EcnfHandle, SolveOptions
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    cfg = CONFIGS[args.config]
+
+    h = EcnfHandle(cfg, init_params(cfg, 0), local)
+    g = torch.Generator(device=dev)
+    g.manual_seed(1234 + rank)                       # each rank samples its own molecules
+    z = torch.randn((args.batch, cfg.event_dim), generator=g, device=dev)
+    x0 = h.base_sample(z)
+    feat = torch.zeros((args.batch, cfg.n_nodes), device=dev, dtype=torch.int32)
+    opts = SolveOptions(solver="euler", step_size=1.0 / args.nfe)
+
+    def step():
+        return h.integrate(x0, feat, 0.0, 1.0, opts, check_status=False)
+
+    for _ in range(args.warmup):
+        y1, _, nfe, _ = step()
+    torch.cuda.synchronize(dev)
+    nfe_seen = int(nfe.max()) if args.warmup else args.nfe
+
+    stream = torch.cuda.current_stream(dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        y1, _, nfe, status = step()
+        ev[i][1].record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    t_max = float(t.item())
+    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    assert int((status != 0).sum()) == 0 and torch.isfinite(y1).all()
+
+    value = world * args.batch * args.steps / t_max
+    F = flops_per_eval(cfg)
+    achieved = F * nfe_seen * args.batch / (kernel_ms * 1e-3) / 1e12
+
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", f"pmc_traffic_{args.config}_b{args.batch}.json")
+    if os.path.exists(pmc):
+        with open(pmc) as f:
+            traffic = json.load(f).get("hbm_bytes_per_launch")
+
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_molecules > 0:
+        threads = args.cpu_threads or len(os.sched_getaffinity(0))
+        rate, secs = cpu_baseline(args.config, args.cpu_molecules, args.nfe, threads)
+        cpu = {"value": rate, "unit": "molecules/s", "cores": threads, "kind": "port",
+               "sample": f"{args.cpu_molecules} LJ13 molecules x {args.nfe} Euler steps, oracle numpy fp32 "
+                         f"batched restatement ({secs:.1f} s)"}
+
+    if rank == 0:
+        out = {
+            "metric": "sampled molecules/sec (fixed-step ODE, NFE=100), LJ13 N=13",
+            "value": value,
+            "unit": "molecules/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": t_max / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (seeded zero-CoM Gaussian x0, flax-default random-init lj13 weights)",
+            "config": {"workload": f"{args.config} sample, Euler NFE={nfe_seen}, batch {args.batch}/GPU",
+                       "n_nodes": cfg.n_nodes, "batch_per_gpu": args.batch, "global_batch": world * args.batch,
+                       "nfe": nfe_seen, "solver": "euler", "parallelism": f"dp{world}"},
+            "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
+                         "frac": achieved / PEAK_FP32_MFMA_TFLOPS, "traffic": traffic,
+                         "kernel": "integrate_kernel", "kernel_ms": kernel_ms,
+                         "flop_per_launch": F * nfe_seen * args.batch},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,873 @@
+// ecnf_hip.hip — libecnf_hip.so: the equivariant-CNF sample / log_prob path on MI355X (gfx950).
+//
+// Kernels
+//   vf_kernel        one EGNN evaluation (+ JVPs) per molecule      <- cnf.apply / jax.vjp
+//   integrate_kernel the whole ODE solve, one launch: each workgroup integrates its MPW molecules end to end
+//                    (Euler / Dopri5 fixed step / Dopri5 + PID per molecule), state in LDS, the EGNN eval
+//                    as a device function                            <- diffrax.diffeqsolve
+//   base kernels     zero-CoM Gaussian projection and log-density    <- distrax Transformed(FlatZeroCoMGaussian)
+// Host
+//   parameter walk of the flat (ravel_pytree-ordered) blob, repacking into MFMA fragment order, C-ABI.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/ecnf.h"
+#include "egnn_eval.hpp"
+
+namespace ecnf {
+
+// ---------------------------------------------------------------------------------------------------
+// Dopri5 tableau (diffrax 2023: Shampine's embedded pair, FSAL)
+// ---------------------------------------------------------------------------------------------------
+__constant__ float kA[6][6] = {
+    {(float)(1.0 / 5), 0, 0, 0, 0, 0},
+    {(float)(3.0 / 40), (float)(9.0 / 40), 0, 0, 0, 0},
+    {(float)(44.0 / 45), (float)(-56.0 / 15), (float)(32.0 / 9), 0, 0, 0},
+    {(float)(19372.0 / 6561), (float)(-25360.0 / 2187), (float)(64448.0 / 6561), (float)(-212.0 / 729), 0, 0},
+    {(float)(9017.0 / 3168), (float)(-355.0 / 33), (float)(46732.0 / 5247), (float)(49.0 / 176),
+     (float)(-5103.0 / 18656), 0},
+    {(float)(35.0 / 384), 0.0f, (float)(500.0 / 1113), (float)(125.0 / 192), (float)(-2187.0 / 6784),
+     (float)(11.0 / 84)}};
+__constant__ float kC[7] = {0.0f, (float)(1.0 / 5), (float)(3.0 / 10), (float)(4.0 / 5), (float)(8.0 / 9), 1.0f, 1.0f};
+__constant__ float kBerr[7] = {(float)(35.0 / 384 - 1951.0 / 21600),
+                               0.0f,
+                               (float)(500.0 / 1113 - 22642.0 / 50085),
+                               (float)(125.0 / 192 - 451.0 / 720),
+                               (float)(-2187.0 / 6784 + 12231.0 / 42400),
+                               (float)(11.0 / 84 - 649.0 / 6300),
+                               (float)(-1.0 / 60.0)};
+
+struct SolveP {
+  int solver, div, adaptive, max_steps;
+  float tau0, tau1, dirf, dt0, rtol, atol, dtmin;
+};
+
+// solver state in LDS, after the eval region
+struct SolverLds {
+  float *ys, *vout, *tin, *tout, *y, *eps, *kx;   // [MPW][ND] each, kx [7][MPW][ND]
+  float *ts, *divv, *lp, *kl, *tau, *tnext, *dt, *h, *l1, *h0;   // [MPW] (kl: [7][MPW])
+  int *active, *atmin, *nfe, *steps, *status, *keep, *any;
+};
+
+__host__ __device__ inline int solver_lds_floats(int MPW, int ND) {
+  return 13 * align4(MPW * ND) + 16 * align4(MPW) + 8 * align4(MPW) + 4;
+}
+
+__device__ inline SolverLds carve_solver(float* p, int MPW, int ND) {
+  SolverLds st;
+  const int a = align4(MPW * ND), b = align4(MPW);
+  st.ys = p; p += a;  st.vout = p; p += a;  st.tin = p; p += a;  st.tout = p; p += a;
+  st.y = p; p += a;   st.eps = p; p += a;   st.kx = p; p += 7 * a;
+  st.ts = p; p += b;  st.divv = p; p += b;  st.lp = p; p += b;   st.kl = p; p += 7 * b;
+  st.tau = p; p += b; st.tnext = p; p += b; st.dt = p; p += b;   st.h = p; p += b;
+  st.l1 = p; p += b;  st.h0 = p; p += b;
+  int* q = reinterpret_cast<int*>(p);
+  st.active = q; q += b; st.atmin = q; q += b; st.nfe = q; q += b; st.steps = q; q += b;
+  st.status = q; q += b; st.keep = q; q += b; st.any = q;
+  return st;
+}
+
+__device__ inline float clip_end(float tn, float tau1) { return tn > tau1 - 1e-6f ? tau1 : tn; }
+
+// one evaluation of the joint field g(tau, y) = dir * f(dir * tau, y) at (st.ts, st.ys) for every molecule
+// of the workgroup; writes kx_out [MPW][ND] and kl_out [MPW].  Exactly one egnn_eval call site (it is inlined).
+template <int NF, int NT, int L, int D>
+__device__ __forceinline__ void joint_field(const Net& net, const Lds& s, const SolverLds& st, const SolveP& sp,
+                                            float* kx_out, float* kl_out) {
+  const int tid = threadIdx.x, MPW = net.MPW, ND = net.ND;
+  // NT == 0: one primal eval; Hutchinson: one JVP along eps; exact: ND JVPs along e_k (trace of J)
+  const int nrep = (NT == 0 || sp.div == ECNF_DIV_HUTCHINSON) ? 1 : ND;
+  if (tid < MPW) st.divv[tid] = 0.f;
+  for (int k = 0; k < nrep; ++k) {
+    if constexpr (NT) {
+      if (sp.div == ECNF_DIV_HUTCHINSON) {
+        for (int i = tid; i < MPW * ND; i += kThreads) st.tin[i] = st.eps[i];
+      } else {
+        for (int i = tid; i < MPW * ND; i += kThreads) st.tin[i] = ((i % ND) == k) ? 1.0f : 0.0f;
+      }
+      __syncthreads();
+    }
+    egnn_eval<NF, NT, L, D>(net, s, st.ys, st.ts, st.tin, st.vout, st.tout);
+    if constexpr (NT) {
+      if (tid < MPW) {
+        if (sp.div == ECNF_DIV_HUTCHINSON) {
+          float acc = 0.f;
+          for (int c = 0; c < ND; ++c) acc += st.tout[tid * ND + c] * st.eps[tid * ND + c];
+          st.divv[tid] = acc;
+        } else {
+          st.divv[tid] += st.tout[tid * ND + k];
+        }
+      }
+    }
+  }
+  for (int i = tid; i < MPW * ND; i += kThreads) kx_out[i] = sp.dirf * st.vout[i];
+  if (tid < MPW) {
+    kl_out[tid] = sp.dirf * st.divv[tid];
+    if (st.active[tid]) st.nfe[tid] += 1;
+  }
+  __syncthreads();
+}
+
+// rms over the (x, logp) leaves of one molecule: sqrt((sum_c a_c^2 + b^2) / (ND + 1))
+__device__ inline float rms_joint(float sumsq_x, float l, int ND) { return sqrtf((sumsq_x + l * l) / (float)(ND + 1)); }
+
+enum Phase { kEuler = 0, kInit0 = 1, kInit1 = 2, kFsal = 3, kStage = 4 };
+
+// The whole solve as a phase machine around ONE field evaluation per loop trip.
+template <int NF, int NT, int L, int D>
+__global__ __launch_bounds__(kThreads) void integrate_kernel(Net net, SolveP sp, const float* __restrict__ y0,
+                                                             const int32_t* __restrict__ feat,
+                                                             const float* __restrict__ eps, float* y1,
+                                                             float* dlogp, int32_t* nfe_out, int32_t* status_out,
+                                                             int B) {
+  extern __shared__ float smem[];
+  const int tid = threadIdx.x, MPW = net.MPW, ND = net.ND, N = net.N;
+  const Lds s = carve_lds<NT>(net, smem);
+  const SolverLds st = carve_solver(s.tail, MPW, ND);
+  const int mol0 = blockIdx.x * MPW;
+  const int nmol = min(MPW, B - mol0);
+  const int a = align4(MPW * ND), b = align4(MPW);
+
+  // zero the eval scratch (aggregates must start at +0; padding rows stay finite)
+  for (int i = tid; i < (int)(s.tail - smem); i += kThreads) smem[i] = 0.f;
+  __syncthreads();
+  for (int i = tid; i < MPW * ND; i += kThreads) {
+    const int m = i / ND;
+    st.y[i] = m < nmol ? y0[(size_t)mol0 * ND + i] : 0.f;
+    st.eps[i] = (m < nmol && eps) ? eps[(size_t)mol0 * ND + i] : 0.f;
+  }
+  for (int i = tid; i < MPW * N; i += kThreads) s.feat[i] = (i / N) < nmol ? feat[(size_t)mol0 * N + i] : 0;
+  if (tid < MPW) {
+    st.lp[tid] = 0.f;
+    st.tau[tid] = sp.tau0;
+    st.active[tid] = tid < nmol ? 1 : 0;
+    st.atmin[tid] = 0;
+    st.nfe[tid] = 0;
+    st.steps[tid] = 0;
+    st.status[tid] = ECNF_OK;
+    st.dt[tid] = sp.dt0;
+    st.tnext[tid] = clip_end(fminf(sp.tau0 + sp.dt0, sp.tau1), sp.tau1);
+  }
+  __syncthreads();
+
+  // Euler: ConstantStepSize, all molecules share the (uniform, register-held) time grid
+  float e_tau = sp.tau0, e_tn = clip_end(sp.tau0 + sp.dt0, sp.tau1), e_h = 0.f;
+  int e_steps = 0;
+  int phase = sp.solver == ECNF_SOLVER_EULER ? kEuler : (sp.adaptive ? kInit0 : kFsal);
+  int stage = 1;
+
+  while (true) {
+    // ------------------------------------------------ inputs of this evaluation
+    float* kx_out;
+    float* kl_out;
+    if (phase == kEuler) {
+      if (!(e_tau < sp.tau1)) break;
+      if (++e_steps > sp.max_steps) {
+        if (tid < nmol) st.status[tid] = ECNF_E_MAX_STEPS;
+        break;
+      }
+      e_h = e_tn - e_tau;
+      for (int i = tid; i < MPW * ND; i += kThreads) st.ys[i] = st.y[i];
+      if (tid < MPW) st.ts[tid] = sp.dirf * e_tau;
+      kx_out = st.kx; kl_out = st.kl;
+    } else if (phase == kInit0 || phase == kFsal) {
+      for (int i = tid; i < MPW * ND; i += kThreads) st.ys[i] = st.y[i];
+      if (tid < MPW) st.ts[tid] = sp.dirf * st.tau[tid];
+      kx_out = st.kx; kl_out = st.kl;
+    } else if (phase == kInit1) {
+      for (int i = tid; i < MPW * ND; i += kThreads) st.ys[i] = st.y[i] + st.h0[i / ND] * st.kx[i];
+      if (tid < MPW) st.ts[tid] = sp.dirf * (st.tau[tid] + st.h0[tid]);
+      kx_out = st.kx + a; kl_out = st.kl + b;
+    } else {
+      if (stage == 1) {
+        if (tid == 0) {
+          int any = 0;
+          for (int m = 0; m < MPW; ++m) any |= st.active[m];
+          *st.any = any;
+        }
+        if (tid < MPW) st.h[tid] = st.tnext[tid] - st.tau[tid];
+        __syncthreads();
+        if (*st.any == 0) break;
+      }
+      for (int i = tid; i < MPW * ND; i += kThreads) {
+        float acc = 0.f;
+        for (int j = 0; j < stage; ++j) acc += kA[stage - 1][j] * st.kx[j * a + i];
+        st.ys[i] = st.y[i] + st.h[i / ND] * acc;
+      }
+      if (tid < MPW) st.ts[tid] = sp.dirf * (st.tau[tid] + kC[stage] * st.h[tid]);
+      kx_out = st.kx + stage * a; kl_out = st.kl + stage * b;
+    }
+    __syncthreads();
+
+    joint_field<NF, NT, L, D>(net, s, st, sp, kx_out, kl_out);
+
+    // ------------------------------------------------ consume it
+    if (phase == kEuler) {
+      for (int i = tid; i < MPW * ND; i += kThreads) st.y[i] = st.y[i] + e_h * st.kx[i];
+      if (tid < MPW) st.lp[tid] = st.lp[tid] + e_h * st.kl[tid];
+      e_tau = e_tn;
+      e_tn = clip_end(e_tau + sp.dt0, sp.tau1);
+    } else if (phase == kInit0) {
+      // Hairer's initial step, part 1 (diffrax _select_initial_step)
+      if (tid < MPW) {
+        float sy = 0.f, sf = 0.f;
+        for (int c = 0; c < ND; ++c) {
+          const float yy = st.y[tid * ND + c];
+          const float sc = sp.atol + fabsf(yy) * sp.rtol;
+          sy += (yy / sc) * (yy / sc);
+          sf += (st.kx[tid * ND + c] / sc) * (st.kx[tid * ND + c] / sc);
+        }
+        const float scl = sp.atol + fabsf(st.lp[tid]) * sp.rtol;
+        const float d0 = rms_joint(sy, st.lp[tid] / scl, ND);
+        const float d1 = rms_joint(sf, st.kl[tid] / scl, ND);
+        const bool cond = (d0 < 1e-5f) || (d1 < 1e-5f);
+        const float d1s = cond ? 1.0f : d1;
+        st.h0[tid] = cond ? 1e-6f : 0.01f * (d0 / d1s);
+        st.l1[tid] = d1;   // stash d1
+      }
+      phase = kInit1;
+    } else if (phase == kInit1) {
+      if (tid < MPW) {
+        float s2 = 0.f;
+        for (int c = 0; c < ND; ++c) {
+          const float sc = sp.atol + fabsf(st.y[tid * ND + c]) * sp.rtol;
+          const float df = (st.kx[a + tid * ND + c] - st.kx[tid * ND + c]) / sc;
+          s2 += df * df;
+        }
+        const float scl = sp.atol + fabsf(st.lp[tid]) * sp.rtol;
+        const float h0 = st.h0[tid];
+        const float d1 = st.l1[tid];
+        const float d2 = rms_joint(s2, (st.kl[b + tid] - st.kl[tid]) / scl, ND) / h0;
+        const float maxd = fmaxf(d1, d2);
+        const float h1 = maxd <= 1e-15f ? fmaxf(1e-6f, h0 * 1e-3f) : powf(0.01f / maxd, 0.2f);
+        const float dt = fminf(100.0f * h0, h1);
+        st.atmin[tid] = dt <= sp.dtmin ? 1 : 0;
+        st.dt[tid] = fmaxf(dt, sp.dtmin);
+        st.tnext[tid] = clip_end(fminf(st.tau[tid] + st.dt[tid], sp.tau1), sp.tau1);
+      }
+      phase = kFsal;
+    } else if (phase == kFsal) {
+      phase = kStage;
+      stage = 1;
+    } else if (stage < 6) {
+      ++stage;
+    } else {
+      // st.ys holds y1 (the stage-7 input uses a_7 = b_sol): error estimate and step control per molecule
+      if (tid < MPW) {
+        const int m = tid;
+        const float h = st.h[m];
+        float accl = 0.f;
+        for (int j = 0; j < 6; ++j) accl += kA[5][j] * st.kl[j * b + m];
+        const float l1 = st.lp[m] + h * accl;
+        st.l1[m] = l1;
+        int keep = 1;
+        float new_dt = sp.dt0;
+        int new_atmin = 0;
+        if (sp.adaptive) {
+          float ssum = 0.f;
+          for (int c = 0; c < ND; ++c) {
+            float e = 0.f;
+            for (int j = 0; j < 7; ++j) e += kBerr[j] * st.kx[j * a + m * ND + c];
+            e = h * e;
+            const float sc = sp.atol + fmaxf(fabsf(st.y[m * ND + c]), fabsf(st.ys[m * ND + c])) * sp.rtol;
+            ssum += (e / sc) * (e / sc);
+          }
+          float el = 0.f;
+          for (int j = 0; j < 7; ++j) el += kBerr[j] * st.kl[j * b + m];
+          el = h * el;
+          const float scl = sp.atol + fmaxf(fabsf(st.lp[m]), fabsf(l1)) * sp.rtol;
+          const float err = rms_joint(ssum, el / scl, ND);
+          keep = (err < 1.0f) || st.atmin[m];
+          const float inv = 1.0f / err;
+          float factor = 0.9f * powf(inv, 0.2f);
+          factor = fminf(fmaxf(factor, keep ? 1.0f : 0.2f), 10.0f);
+          if (isnan(factor)) factor = 1.0f;
+          new_dt = h * factor;
+          new_atmin = new_dt <= sp.dtmin ? 1 : 0;
+          new_dt = fmaxf(new_dt, sp.dtmin);
+        }
+        st.keep[m] = keep && st.active[m];
+        st.dt[m] = new_dt;
+        st.h0[m] = (float)new_atmin;
+      }
+      __syncthreads();
+      for (int i = tid; i < MPW * ND; i += kThreads) {
+        const int m = i / ND;
+        if (st.keep[m]) {
+          st.y[i] = st.ys[i];
+          st.kx[i] = st.kx[6 * a + i];
+        }
+      }
+      if (tid < MPW) {
+        const int m = tid;
+        if (st.active[m]) {
+          if (st.keep[m]) {
+            st.lp[m] = st.l1[m];
+            st.kl[m] = st.kl[6 * b + m];
+            st.tau[m] = st.tnext[m];
+          }
+          st.atmin[m] = (int)st.h0[m];
+          st.steps[m] += 1;
+          st.tnext[m] = sp.adaptive ? clip_end(fminf(st.tau[m] + st.dt[m], sp.tau1), sp.tau1)
+                                    : clip_end(st.tau[m] + sp.dt0, sp.tau1);
+          if (!(st.tau[m] < sp.tau1)) {
+            st.active[m] = 0;
+          } else if (st.steps[m] >= sp.max_steps) {
+            st.status[m] = ECNF_E_MAX_STEPS;
+            st.active[m] = 0;
+          }
+        }
+      }
+      stage = 1;
+    }
+    __syncthreads();
+  }
+  __syncthreads();
+  for (int i = tid; i < nmol * ND; i += kThreads) y1[(size_t)mol0 * ND + i] = st.y[i];
+  if (tid < nmol) {
+    if (dlogp) dlogp[mol0 + tid] = st.lp[tid];
+    if (nfe_out) nfe_out[mol0 + tid] = st.nfe[tid];
+    if (status_out) status_out[mol0 + tid] = st.status[tid];
+  }
+}
+
+// one evaluation (and n_tangents JVPs) per molecule
+template <int NF, int NT, int L, int D>
+__global__ __launch_bounds__(kThreads) void vf_kernel(Net net, const float* __restrict__ x, const float* __restrict__ t,
+                                                      const int32_t* __restrict__ feat,
+                                                      const float* __restrict__ tan_in, int ntan, float* v,
+                                                      float* tan_out, int B) {
+  extern __shared__ float smem[];
+  const int tid = threadIdx.x, MPW = net.MPW, ND = net.ND, N = net.N;
+  const Lds s = carve_lds<NT>(net, smem);
+  const SolverLds st = carve_solver(s.tail, MPW, ND);
+  const int mol0 = blockIdx.x * MPW;
+  const int nmol = min(MPW, B - mol0);
+  for (int i = tid; i < (int)(s.tail - smem); i += kThreads) smem[i] = 0.f;
+  __syncthreads();
+  for (int i = tid; i < MPW * ND; i += kThreads) st.ys[i] = (i / ND) < nmol ? x[(size_t)mol0 * ND + i] : 0.f;
+  for (int i = tid; i < MPW * N; i += kThreads) s.feat[i] = (i / N) < nmol ? feat[(size_t)mol0 * N + i] : 0;
+  if (tid < MPW) st.ts[tid] = tid < nmol ? t[mol0 + tid] : 0.f;
+  __syncthreads();
+  if constexpr (NT == 0) {
+    egnn_eval<NF, 0, L, D>(net, s, st.ys, st.ts, nullptr, st.vout, nullptr);
+    for (int i = tid; i < nmol * ND; i += kThreads) v[(size_t)mol0 * ND + i] = st.vout[i];
+  } else {
+    for (int k = 0; k < ntan; ++k) {
+      for (int i = tid; i < MPW * ND; i += kThreads) {
+        const int m = i / ND, c = i - m * ND;
+        st.tin[i] = m < nmol ? tan_in[((size_t)(mol0 + m) * ntan + k) * ND + c] : 0.f;
+      }
+      __syncthreads();
+      egnn_eval<NF, 1, L, D>(net, s, st.ys, st.ts, st.tin, st.vout, st.tout);
+      for (int i = tid; i < nmol * ND; i += kThreads) {
+        const int m = i / ND, c = i - m * ND;
+        tan_out[((size_t)(mol0 + m) * ntan + k) * ND + c] = st.tout[i];
+        if (k == 0 && v) v[(size_t)mol0 * ND + i] = st.vout[i];
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// x0 = s * (z - mean_nodes z)   (zero_com_base.py:88-93, build_cnf.py:46)
+__global__ void base_sample_kernel(const float* __restrict__ z, float* x0, int B, int N, int D, float scale) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;   // (b, d)
+  if (idx >= B * D) return;
+  const int bb = idx / D, d = idx - bb * D;
+  const float* zb = z + (size_t)bb * N * D;
+  float acc = 0.f;
+  for (int i = 0; i < N; ++i) acc += zb[i * D + d];
+  const float mean = acc / (float)N;
+  for (int i = 0; i < N; ++i) x0[(size_t)bb * N * D + i * D + d] = scale * (zb[i * D + d] - mean);
+}
+
+// log N_{(N-1)D}(remove_mean(y / s)) - (N-1) D log s   (zero_com_base.py:64-84, build_cnf.py:50-57)
+__global__ void base_log_prob_kernel(const float* __restrict__ y, float* out, int B, int N, int D, float scale) {
+  const int bb = blockIdx.x * blockDim.x + threadIdx.x;
+  if (bb >= B) return;
+  const float* yb = y + (size_t)bb * N * D;
+  const float inv = 1.0f / scale;
+  float mean[3] = {0.f, 0.f, 0.f};
+  for (int i = 0; i < N; ++i)
+    for (int d = 0; d < D; ++d) mean[d] += yb[i * D + d] * inv;
+  for (int d = 0; d < D; ++d) mean[d] /= (float)N;
+  float r2 = 0.f;
+  for (int i = 0; i < N; ++i)
+    for (int d = 0; d < D; ++d) {
+      const float u = yb[i * D + d] * inv - mean[d];
+      r2 += u * u;
+    }
+  const int dof = (N - 1) * D;
+  const float log_norm = -0.5f * (float)dof * logf(2.0f * 3.14159265358979f);
+  const float ildj = -(float)(N * D) * logf(scale) * (float)(N - 1) / (float)N;
+  out[bb] = -0.5f * r2 + log_norm + ildj;
+}
+
+}  // namespace ecnf
+
+// =====================================================================================================
+// host side
+// =====================================================================================================
+using namespace ecnf;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                         \
+  do {                                                                                        \
+    hipError_t e_ = (expr);                                                                   \
+    if (e_ != hipSuccess) return fail(ECNF_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+int check_cfg(const ecnf_cfg* c) {
+  if (!c) return fail(ECNF_E_INVALID, "cfg is NULL");
+  if (c->n_nodes < 2 || c->n_nodes > 33)
+    return fail(ECNF_E_UNSUPPORTED, "n_nodes must be in [2, 33] (a receiver's N-1 edges must fit one 32-edge tile)");
+  if (c->dim != 2 && c->dim != 3) return fail(ECNF_E_UNSUPPORTED, "dim must be 2 or 3");
+  if (c->n_features < 1) return fail(ECNF_E_INVALID, "n_features must be >= 1");
+  if (c->hidden < 32 || c->hidden % 32) return fail(ECNF_E_UNSUPPORTED, "hidden must be a multiple of 32");
+  if (c->time_embedding_dim < 4 || c->time_embedding_dim > 2 * kMaxHalfT || c->time_embedding_dim % 2)
+    return fail(ECNF_E_UNSUPPORTED, "time_embedding_dim must be even and in [4, 16]");
+  if (c->mlp_width != 64 && c->mlp_width != 128 && c->mlp_width != 256)
+    return fail(ECNF_E_UNSUPPORTED, "mlp_width must be 64, 128 or 256");
+  if (c->mlp_depth < 2 || c->mlp_depth > 4) return fail(ECNF_E_UNSUPPORTED, "mlp_depth must be in [2, 4]");
+  if (c->n_blocks < 1 || c->n_blocks > kMaxBlocks) return fail(ECNF_E_UNSUPPORTED, "n_blocks must be in [1, 10]");
+  if (!(c->base_scale > 0.f)) return fail(ECNF_E_INVALID, "base_scale must be > 0");
+  return ECNF_OK;
+}
+
+size_t param_count(const ecnf_cfg& c) {
+  const size_t H = c.hidden, T = c.time_embedding_dim, M = c.mlp_width, L = c.mlp_depth, K = c.n_blocks;
+  size_t per_block = 2 * (1 + M);                                 // Dense_0, Dense_1
+  per_block += (2 * H + 1) * M + M + (L - 1) * (M * M + M);      // phi_e
+  per_block += (M + H) * M + M + (L - 1) * (M * M + M) + M * H + H;  // phi_h
+  per_block += L * (M * M + M);                                   // phi_x_torso
+  per_block += (H + T) * H + H;                                   // EGNN_0/Dense_k
+  return K * per_block + 1 + (size_t)c.n_features * H;
+}
+
+}  // namespace
+
+struct ecnf_handle {
+  ecnf_cfg cfg;
+  int device;
+  float* dbuf;
+  Net net[2];          // [NT]
+  size_t lds[2];       // dynamic LDS bytes per workgroup [NT]
+};
+
+namespace {
+
+struct Packer {
+  std::vector<float> buf;
+  size_t put(const float* src, size_t n) {
+    size_t off = (buf.size() + 15) & ~size_t(15);   // 64-byte alignment
+    buf.resize(off + n, 0.f);
+    if (src) std::memcpy(buf.data() + off, src, n * sizeof(float));
+    return off;
+  }
+};
+
+struct HostBlock {
+  const float *xb, *xk, *gb, *gk;
+  const float *eb[4], *ek[4];
+  const float *hb[5], *hk[5];
+  const float *tb[4], *tk[4];
+  const float *nb, *nk;
+};
+
+int choose_mpw(const ecnf_cfg& c, int NT, int* mpw_out, size_t* lds_out, int* rp_out) {
+  const int N = c.n_nodes, D = c.dim, H = c.hidden, T = c.time_embedding_dim, M = c.mlp_width;
+  const int E = N * (N - 1);
+  const char* env = std::getenv(NT ? "ECNF_MPW_TANGENT" : "ECNF_MPW");
+  const int forced = env ? std::atoi(env) : 0;
+  double best = -1;
+  int best_m = 0;
+  size_t best_lds = 0;
+  int best_rp = 0;
+  for (int m = 1; m <= 32; ++m) {
+    const int RP = 32 * ((m * N + 31) / 32);
+    const int floats = (NT ? lds_eval_floats<1>(N, D, H, T, M, m, RP) : lds_eval_floats<0>(N, D, H, T, M, m, RP)) +
+                       solver_lds_floats(m, N * D);
+    const size_t bytes = (size_t)floats * 4;
+    if (bytes > 160 * 1024) break;
+    const int EP = 32 * ((E + 31) / 32);
+    const int tiles = m * EP / 32;
+    const double eff = (double)tiles / (kWaves * ((tiles + kWaves - 1) / kWaves)) * (double)(m * E) / (tiles * 32.0);
+    if (forced ? m == forced : eff > best + 1e-9) {
+      best = eff;
+      best_m = m;
+      best_lds = bytes;
+      best_rp = RP;
+    }
+    if (forced && m == forced) break;
+  }
+  if (!best_m) return fail(ECNF_E_UNSUPPORTED, "configuration does not fit the 160 KiB LDS of one CU");
+  *mpw_out = best_m;
+  *lds_out = best_lds;
+  *rp_out = best_rp;
+  return ECNF_OK;
+}
+
+// ---- kernel dispatch over the compiled shapes (M, L, D) ----
+template <int NF, int NT, int L, int D>
+hipError_t launch_integrate(const ecnf_handle* h, const SolveP& sp, const float* y0, const int32_t* feat,
+                            const float* eps, float* y1, float* dlogp, int32_t* nfe, int32_t* status, int B,
+                            hipStream_t stream) {
+  auto k = integrate_kernel<NF, NT, L, D>;
+  hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds[NT]);
+  if (e != hipSuccess) return e;
+  const int grid = (B + h->net[NT].MPW - 1) / h->net[NT].MPW;
+  hipLaunchKernelGGL(k, dim3(grid), dim3(kThreads), h->lds[NT], stream, h->net[NT], sp, y0, feat, eps, y1, dlogp,
+                     nfe, status, B);
+  return hipGetLastError();
+}
+
+template <int NF, int NT, int L, int D>
+hipError_t launch_vf(const ecnf_handle* h, const float* x, const float* t, const int32_t* feat, const float* tan_in,
+                     int ntan, float* v, float* tan_out, int B, hipStream_t stream) {
+  auto k = vf_kernel<NF, NT, L, D>;
+  hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds[NT]);
+  if (e != hipSuccess) return e;
+  const int grid = (B + h->net[NT].MPW - 1) / h->net[NT].MPW;
+  hipLaunchKernelGGL(k, dim3(grid), dim3(kThreads), h->lds[NT], stream, h->net[NT], x, t, feat, tan_in, ntan, v,
+                     tan_out, B);
+  return hipGetLastError();
+}
+
+// compiled shapes: (M, L, D) with tangent support where registers allow (M <= 128)
+#define ECNF_SHAPES(X)  \
+  X(128, 3, 3)          \
+  X(128, 3, 2)          \
+  X(128, 2, 3)          \
+  X(128, 2, 2)          \
+  X(64, 2, 3)           \
+  X(64, 2, 2)           \
+  X(64, 3, 3)           \
+  X(64, 3, 2)
+
+#define ECNF_SHAPES_PRIMAL_ONLY(X) \
+  X(256, 4, 3)                     \
+  X(256, 3, 3)
+
+bool shape_supported(const ecnf_cfg& c, int NT) {
+  const int M = c.mlp_width, L = c.mlp_depth, D = c.dim;
+#define X(m, l, d) \
+  if (M == m && L == l && D == d) return true;
+  ECNF_SHAPES(X)
+#undef X
+  if (NT) return false;
+#define X(m, l, d) \
+  if (M == m && L == l && D == d) return true;
+  ECNF_SHAPES_PRIMAL_ONLY(X)
+#undef X
+  return false;
+}
+
+hipError_t dispatch_integrate(const ecnf_handle* h, int NT, const SolveP& sp, const float* y0, const int32_t* feat,
+                              const float* eps, float* y1, float* dlogp, int32_t* nfe, int32_t* status, int B,
+                              hipStream_t stream) {
+  const int M = h->cfg.mlp_width, L = h->cfg.mlp_depth, D = h->cfg.dim;
+#define X(m, l, d)                                                                                        \
+  if (M == m && L == l && D == d)                                                                         \
+    return NT ? launch_integrate<m / 32, 1, l, d>(h, sp, y0, feat, eps, y1, dlogp, nfe, status, B, stream) \
+              : launch_integrate<m / 32, 0, l, d>(h, sp, y0, feat, eps, y1, dlogp, nfe, status, B, stream);
+  ECNF_SHAPES(X)
+#undef X
+#define X(m, l, d) \
+  if (M == m && L == l && D == d && !NT) return launch_integrate<m / 32, 0, l, d>(h, sp, y0, feat, eps, y1, dlogp, nfe, status, B, stream);
+  ECNF_SHAPES_PRIMAL_ONLY(X)
+#undef X
+  return hipErrorInvalidValue;
+}
+
+hipError_t dispatch_vf(const ecnf_handle* h, int NT, const float* x, const float* t, const int32_t* feat,
+                       const float* tan_in, int ntan, float* v, float* tan_out, int B, hipStream_t stream) {
+  const int M = h->cfg.mlp_width, L = h->cfg.mlp_depth, D = h->cfg.dim;
+#define X(m, l, d)                                                                           \
+  if (M == m && L == l && D == d)                                                            \
+    return NT ? launch_vf<m / 32, 1, l, d>(h, x, t, feat, tan_in, ntan, v, tan_out, B, stream) \
+              : launch_vf<m / 32, 0, l, d>(h, x, t, feat, tan_in, ntan, v, tan_out, B, stream);
+  ECNF_SHAPES(X)
+#undef X
+#define X(m, l, d) \
+  if (M == m && L == l && D == d && !NT) return launch_vf<m / 32, 0, l, d>(h, x, t, feat, tan_in, ntan, v, tan_out, B, stream);
+  ECNF_SHAPES_PRIMAL_ONLY(X)
+#undef X
+  return hipErrorInvalidValue;
+}
+
+}  // namespace
+
+// =====================================================================================================
+// C-ABI
+// =====================================================================================================
+extern "C" {
+
+int ecnf_abi_version(void) { return ECNF_ABI_VERSION; }
+
+const char* ecnf_last_error(void) { return g_err.c_str(); }
+
+int ecnf_param_count(const ecnf_cfg* cfg, size_t* n_floats) {
+  int rc = check_cfg(cfg);
+  if (rc) return rc;
+  if (!n_floats) return fail(ECNF_E_INVALID, "n_floats is NULL");
+  *n_floats = param_count(*cfg);
+  g_err.clear();
+  return ECNF_OK;
+}
+
+int ecnf_create(const ecnf_cfg* cfg, const float* params, size_t n_floats, int device, ecnf_handle** out) {
+  int rc = check_cfg(cfg);
+  if (rc) return rc;
+  if (!params || !out) return fail(ECNF_E_INVALID, "params/out is NULL");
+  const ecnf_cfg c = *cfg;
+  if (n_floats != param_count(c))
+    return fail(ECNF_E_INVALID, "params blob has " + std::to_string(n_floats) + " floats, expected " +
+                                    std::to_string(param_count(c)));
+  if (!shape_supported(c, 0))
+    return fail(ECNF_E_UNSUPPORTED, "no kernel compiled for mlp_width=" + std::to_string(c.mlp_width) +
+                                        " mlp_depth=" + std::to_string(c.mlp_depth) + " dim=" + std::to_string(c.dim));
+  const int H = c.hidden, T = c.time_embedding_dim, M = c.mlp_width, L = c.mlp_depth, K = c.n_blocks;
+  const int NF = M / 32;
+
+  // ---- walk the ravel_pytree-ordered blob ----
+  std::vector<HostBlock> hb(K);
+  const float* p = params;
+  auto take = [&](size_t n) {
+    const float* q = p;
+    p += n;
+    return q;
+  };
+  for (int k = 0; k < K; ++k) {   // EGNN_0/{k} in sorted order (K <= 10 so lexicographic == numeric)
+    HostBlock& b = hb[k];
+    b.xb = take(1); b.xk = take(M);
+    b.gb = take(1); b.gk = take(M);
+    for (int l = 0; l < L; ++l) { b.eb[l] = take(M); b.ek[l] = take((size_t)(l == 0 ? 2 * H + 1 : M) * M); }
+    for (int l = 0; l <= L; ++l) {
+      const int out_f = l == L ? H : M, in_f = l == 0 ? M + H : M;
+      b.hb[l] = take(out_f); b.hk[l] = take((size_t)in_f * out_f);
+    }
+    for (int l = 0; l < L; ++l) { b.tb[l] = take(M); b.tk[l] = take((size_t)M * M); }
+  }
+  for (int k = 0; k < K; ++k) { hb[k].nb = take(H); hb[k].nk = take((size_t)(H + T) * H); }
+  const float fs = *take(1);
+  const float* emb = take((size_t)c.n_features * H);
+  if ((size_t)(p - params) != n_floats) return fail(ECNF_E_INVALID, "internal: param walk size mismatch");
+
+  // ---- repack ----
+  Packer pk;
+  struct Off { size_t Wn, bn, Wp, bp, wd, We, be, wx, wg, Wh[kMaxPhiH], bh[kMaxPhiH]; float bx, bg; };
+  std::vector<Off> off(K);
+  for (int k = 0; k < K; ++k) {
+    const HostBlock& b = hb[k];
+    Off& o = off[k];
+    o.Wn = pk.put(b.nk, (size_t)(H + T) * H);
+    o.bn = pk.put(b.nb, H);
+    std::vector<float> wp((size_t)H * 2 * M), bp(2 * M, 0.f), wd(M);
+    for (int r = 0; r < H; ++r)
+      for (int j = 0; j < M; ++j) {
+        wp[(size_t)r * 2 * M + j] = b.ek[0][(size_t)r * M + j];             // sender rows 0..H-1
+        wp[(size_t)r * 2 * M + M + j] = b.ek[0][(size_t)(H + r) * M + j];   // receiver rows H..2H-1
+      }
+    for (int j = 0; j < M; ++j) { bp[M + j] = b.eb[0][j]; wd[j] = b.ek[0][(size_t)2 * H * M + j]; }
+    o.Wp = pk.put(wp.data(), wp.size());
+    o.bp = pk.put(bp.data(), bp.size());
+    o.wd = pk.put(wd.data(), wd.size());
+    // chain: phi_e.1..L-1, phi_x.0..L-1, each [M][M] -> fragment order
+    const int nchain = 2 * L - 1;
+    std::vector<float> we((size_t)nchain * M * M), be((size_t)nchain * M);
+    for (int cl = 0; cl < nchain; ++cl) {
+      const float* W = cl < L - 1 ? b.ek[cl + 1] : b.tk[cl - (L - 1)];
+      const float* bb = cl < L - 1 ? b.eb[cl + 1] : b.tb[cl - (L - 1)];
+      float* dst = we.data() + (size_t)cl * M * M;
+      for (int jb = 0; jb < NF; ++jb)
+        for (int fb = 0; fb < NF; ++fb)
+          for (int q = 0; q < 4; ++q)
+            for (int l = 0; l < 64; ++l)
+              for (int e = 0; e < 4; ++e) {
+                const int krow = fb * 32 + e + 8 * q + 4 * (l >> 5);
+                const int col = jb * 32 + (l & 31);
+                dst[((((size_t)jb * NF + fb) * 4 + q) * 64 + l) * 4 + e] = W[(size_t)krow * M + col];
+              }
+      std::memcpy(be.data() + (size_t)cl * M, bb, M * sizeof(float));
+    }
+    o.We = pk.put(we.data(), we.size());
+    o.be = pk.put(be.data(), be.size());
+    o.wx = pk.put(b.xk, M);
+    o.wg = pk.put(b.gk, M);
+    o.bx = *b.xb;
+    o.bg = *b.gb;
+    for (int l = 0; l <= L; ++l) {
+      const int out_f = l == L ? H : M, in_f = l == 0 ? M + H : M;
+      o.Wh[l] = pk.put(b.hk[l], (size_t)in_f * out_f);
+      o.bh[l] = pk.put(b.hb[l], out_f);
+    }
+  }
+  const size_t off_emb = pk.put(emb, (size_t)c.n_features * H);
+
+  int ndev = 0;
+  HIP_TRY(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev) return fail(ECNF_E_INVALID, "device index out of range");
+  HIP_TRY(hipSetDevice(device));
+  float* dbuf = nullptr;
+  HIP_TRY(hipMalloc(&dbuf, pk.buf.size() * sizeof(float)));
+  HIP_TRY(hipMemcpy(dbuf, pk.buf.data(), pk.buf.size() * sizeof(float), hipMemcpyHostToDevice));
+
+  ecnf_handle* h = new ecnf_handle();
+  h->cfg = c;
+  h->device = device;
+  h->dbuf = dbuf;
+  for (int NT = 0; NT < 2; ++NT) {
+    Net& n = h->net[NT];
+    std::memset(&n, 0, sizeof(Net));
+    n.N = c.n_nodes; n.D = c.dim; n.H = H; n.T = T; n.M = M; n.L = L; n.K = K; n.nfeat = c.n_features;
+    n.E = c.n_nodes * (c.n_nodes - 1);
+    n.EP = 32 * ((n.E + 31) / 32);
+    n.ND = c.n_nodes * c.dim;
+    n.C = c.normalization_constant;
+    n.fs = fs;
+    n.nn1 = (float)(c.n_nodes - 1);
+    n.sqrt_nn1 = std::sqrt((float)(c.n_nodes - 1));
+    const int half = T / 2;
+    const float ex = std::log(10000.0f) / (float)(half - 1);
+    for (int k = 0; k < half; ++k) n.freqs[k] = std::exp((float)k * -ex);
+    n.emb = dbuf + off_emb;
+    for (int k = 0; k < K; ++k) {
+      BlockW& w = n.blk[k];
+      const Off& o = off[k];
+      w.Wn = dbuf + o.Wn; w.bn = dbuf + o.bn; w.Wp = dbuf + o.Wp; w.bp = dbuf + o.bp; w.wd = dbuf + o.wd;
+      w.We = dbuf + o.We; w.be = dbuf + o.be; w.wx = dbuf + o.wx; w.wg = dbuf + o.wg; w.bx = o.bx; w.bg = o.bg;
+      for (int l = 0; l <= L; ++l) { w.Wh[l] = dbuf + o.Wh[l]; w.bh[l] = dbuf + o.bh[l]; }
+    }
+    int mpw = 0, rp = 0;
+    size_t lds = 0;
+    if (shape_supported(c, NT) && choose_mpw(c, NT, &mpw, &lds, &rp) == ECNF_OK) {
+      n.MPW = mpw;
+      n.RP = rp;
+      h->lds[NT] = lds;
+    } else {
+      n.MPW = 0;
+      h->lds[NT] = 0;
+    }
+  }
+  if (h->net[0].MPW == 0) {
+    hipFree(dbuf);
+    delete h;
+    return fail(ECNF_E_UNSUPPORTED, "configuration does not fit the LDS budget");
+  }
+  *out = h;
+  g_err.clear();
+  return ECNF_OK;
+}
+
+int ecnf_destroy(ecnf_handle* h) {
+  if (!h) return ECNF_OK;
+  HIP_TRY(hipSetDevice(h->device));
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipFree(h->dbuf));
+  delete h;
+  return ECNF_OK;
+}
+
+int ecnf_molecules_per_workgroup(ecnf_handle* h, int32_t with_tangent, int32_t* mpw) {
+  if (!h || !mpw) return fail(ECNF_E_INVALID, "NULL argument");
+  *mpw = h->net[with_tangent ? 1 : 0].MPW;
+  return ECNF_OK;
+}
+
+int ecnf_vector_field(ecnf_handle* h, const float* x, const float* t, const int32_t* feat, float* v, int32_t batch,
+                      void* stream) {
+  if (!h || !x || !t || !feat || !v) return fail(ECNF_E_INVALID, "NULL argument");
+  if (batch < 0) return fail(ECNF_E_INVALID, "batch < 0");
+  if (batch == 0) return ECNF_OK;
+  HIP_TRY(hipSetDevice(h->device));
+  HIP_TRY(dispatch_vf(h, 0, x, t, feat, nullptr, 0, v, nullptr, batch, (hipStream_t)stream));
+  g_err.clear();
+  return ECNF_OK;
+}
+
+int ecnf_vf_jvp(ecnf_handle* h, const float* x, const float* t, const int32_t* feat, const float* tan_in,
+                int32_t n_tangents, float* v, float* tan_out, int32_t batch, void* stream) {
+  if (!h || !x || !t || !feat || !tan_in || !tan_out) return fail(ECNF_E_INVALID, "NULL argument");
+  if (batch < 0 || n_tangents < 1) return fail(ECNF_E_INVALID, "batch < 0 or n_tangents < 1");
+  if (h->net[1].MPW == 0)
+    return fail(ECNF_E_UNSUPPORTED, "no tangent kernel for mlp_width=" + std::to_string(h->cfg.mlp_width));
+  if (batch == 0) return ECNF_OK;
+  HIP_TRY(hipSetDevice(h->device));
+  HIP_TRY(dispatch_vf(h, 1, x, t, feat, tan_in, n_tangents, v, tan_out, batch, (hipStream_t)stream));
+  g_err.clear();
+  return ECNF_OK;
+}
+
+int ecnf_integrate(ecnf_handle* h, const ecnf_solve_opts* o, const float* y0, const int32_t* feat, const float* eps,
+                   float* y1, float* dlogp, int32_t* nfe, int32_t* status, int32_t batch, void* stream) {
+  if (!h || !o || !y0 || !feat || !y1) return fail(ECNF_E_INVALID, "NULL argument");
+  if (batch < 0) return fail(ECNF_E_INVALID, "batch < 0");
+  if (o->solver != ECNF_SOLVER_EULER && o->solver != ECNF_SOLVER_DOPRI5) return fail(ECNF_E_INVALID, "unknown solver");
+  if (o->divergence < ECNF_DIV_NONE || o->divergence > ECNF_DIV_EXACT) return fail(ECNF_E_INVALID, "unknown divergence");
+  if (o->divergence == ECNF_DIV_HUTCHINSON && !eps) return fail(ECNF_E_INVALID, "Hutchinson divergence needs eps");
+  if (o->divergence != ECNF_DIV_NONE && !dlogp) return fail(ECNF_E_INVALID, "divergence requested but dlogp is NULL");
+  if (o->t0 == o->t1) return fail(ECNF_E_INVALID, "t0 == t1");
+  const bool adaptive = !(o->dt0 > 0.f);
+  if (adaptive && o->solver == ECNF_SOLVER_EULER) return fail(ECNF_E_INVALID, "Euler has no error estimate: give dt0 > 0");
+  if (adaptive && !(o->rtol > 0.f && o->atol > 0.f)) return fail(ECNF_E_INVALID, "adaptive stepping needs rtol, atol > 0");
+  if (o->max_steps < 1) return fail(ECNF_E_INVALID, "max_steps < 1");
+  const int NT = o->divergence == ECNF_DIV_NONE ? 0 : 1;
+  if (NT && h->net[1].MPW == 0)
+    return fail(ECNF_E_UNSUPPORTED, "no tangent kernel for mlp_width=" + std::to_string(h->cfg.mlp_width));
+  if (batch == 0) return ECNF_OK;
+  SolveP sp;
+  sp.solver = o->solver;
+  sp.div = o->divergence;
+  sp.adaptive = adaptive ? 1 : 0;
+  sp.max_steps = o->max_steps;
+  sp.dirf = o->t1 > o->t0 ? 1.0f : -1.0f;
+  sp.tau0 = sp.dirf * o->t0;
+  sp.tau1 = sp.dirf * o->t1;
+  sp.dt0 = adaptive ? 0.f : std::fabs(o->dt0);
+  sp.rtol = o->rtol;
+  sp.atol = o->atol;
+  sp.dtmin = o->dtmin;
+  HIP_TRY(hipSetDevice(h->device));
+  HIP_TRY(dispatch_integrate(h, NT, sp, y0, feat, eps, y1, dlogp, nfe, status, batch, (hipStream_t)stream));
+  g_err.clear();
+  return ECNF_OK;
+}
+
+int ecnf_base_sample(ecnf_handle* h, const float* z, float* x0, int32_t batch, void* stream) {
+  if (!h || !z || !x0) return fail(ECNF_E_INVALID, "NULL argument");
+  if (batch <= 0) return batch == 0 ? ECNF_OK : fail(ECNF_E_INVALID, "batch < 0");
+  HIP_TRY(hipSetDevice(h->device));
+  const int n = batch * h->cfg.dim;
+  hipLaunchKernelGGL(base_sample_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, z, x0, batch,
+                     h->cfg.n_nodes, h->cfg.dim, h->cfg.base_scale);
+  HIP_TRY(hipGetLastError());
+  return ECNF_OK;
+}
+
+int ecnf_base_log_prob(ecnf_handle* h, const float* y, float* log_p, int32_t batch, void* stream) {
+  if (!h || !y || !log_p) return fail(ECNF_E_INVALID, "NULL argument");
+  if (batch <= 0) return batch == 0 ? ECNF_OK : fail(ECNF_E_INVALID, "batch < 0");
+  HIP_TRY(hipSetDevice(h->device));
+  hipLaunchKernelGGL(base_log_prob_kernel, dim3((batch + 255) / 256), dim3(256), 0, (hipStream_t)stream, y, log_p,
+                     batch, h->cfg.n_nodes, h->cfg.dim, h->cfg.base_scale);
+  HIP_TRY(hipGetLastError());
+  return ECNF_OK;
+}
+
+}  // extern "C"

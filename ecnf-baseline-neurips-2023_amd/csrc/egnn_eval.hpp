@@ -1,0 +1,581 @@
+// egnn_eval.hpp — one EGNN vector-field evaluation for the MPW molecules of a workgroup (gfx950 / CDNA4).
+//
+// Restates FlatEgnn.__call__ (ecnf/cnf/build_cnf.py:68-93), EGNN.call_single (ecnf/nets/egnn.py:144-190)
+// and EGCL.__call__ (ecnf/nets/egnn.py:49-114) of the reference, with forward-mode tangents (NT = 1) for the
+// divergence terms of ecnf/cnf/sample_and_log_prob.py:57-78.
+//
+// Layout (per workgroup = 4 waves = 256 threads, MPW molecules):
+//   * node rows: molecule m, atom i -> row n = m*N + i, padded to RP = 32*ceil(MPW*N/32); tangent row of n is
+//     RP + n.  All node state lives in LDS as [row][feature] with odd leading dimensions (conflict-free
+//     column reads by 32 lanes).
+//   * node GEMMs (Dense layers on node rows) run on v_mfma_f32_32x32x2_f32 in transposed form
+//     Y^T[j][n] = sum_k W[k][j] X^T[k][n]: A = weights (global, L2-resident), B = node rows (LDS), one output
+//     32x32 tile per (32-output block, 32-node tile); the tangent tile shares every A fragment.
+//   * edge MLPs: edge e (receiver-major, graph.py:6-14) of a molecule sits on MFMA column (lane & 31) of a
+//     32-edge tile; a molecule owns EP = 32*ceil(N(N-1)/32) edge slots starting on a tile boundary.  A whole tile's activation is 16*M/32 registers per lane
+//     and the MFMA accumulator of layer l IS the B operand of layer l+1 (register r of output block fb is the
+//     k-step (fb, r)), so phi_e layers 2..L and all phi_x layers chain with zero LDS traffic; weights are
+//     pre-packed on the host into lane order (one dwordx4 per lane = 4 A fragments).
+//   * phi_e layer 1 is factorised: [h_s | h_r | d^2] W = (h W_s)[s] + (h W_r + b)[r] + d^2 w_d; the per-node
+//     halves are one node GEMM into LDS and are gathered per edge.
+//   * segment sums (e3nn.scatter_sum over the contiguous receiver runs) are segmented suffix scans with
+//     __shfl_down inside each 32-edge tile followed by one LDS add per (segment, tile); a node's N-1 <= 32 edges
+//     touch at most two tiles and 0 + a + b == 0 + b + a, so the result is run-to-run deterministic.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ecnf {
+
+constexpr int kWaves = 4;
+constexpr int kThreads = 64 * kWaves;
+constexpr int kMaxBlocks = 10;
+constexpr int kMaxPhiH = 5;     // L + 1 <= 5
+constexpr int kMaxHalfT = 8;    // T <= 16
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+struct BlockW {
+  const float* Wn;  const float* bn;    // node Dense [(H+T)][H], [H]           (egnn.py:166-167)
+  const float* Wp;  const float* bp;    // [H][2M] = [W_send | W_recv] of phi_e.0, bias [2M] = [0 | b]
+  const float* wd;                      // [M]  phi_e.0 kernel row 2H (the |r|^2 feature)
+  const float* We;  const float* be;    // packed chain weights: phi_e.1..L-1 then phi_x.0..L-1, biases [(2L-1)][M]
+  const float* wx;  const float* wg;    // [M] phi_x output Dense(1) kernel, [M] gate Dense(1) kernel
+  float bx, bg;                         // their biases
+  const float* Wh[kMaxPhiH]; const float* bh[kMaxPhiH];  // phi_h layers, row-major [in][out]
+};
+
+struct Net {
+  int N, D, H, T, M, L, K, nfeat;
+  int E;          // N (N - 1)
+  int EP;         // edges per molecule padded to a multiple of 32 (every molecule starts on a tile boundary)
+  int MPW;        // molecules per workgroup
+  int RP;         // padded primal node rows
+  int ND;         // N * D
+  float C;        // EGCL normalization constant
+  float fs;       // EGNN final_scaling
+  float nn1;      // avg_num_neighbours = N - 1
+  float sqrt_nn1; // sqrt(N - 1) in fp32
+  float freqs[kMaxHalfT];
+  const float* emb;
+  BlockW blk[kMaxBlocks];
+};
+
+// ---------------------------------------------------------------------------------------------------
+// LDS carve-up
+// ---------------------------------------------------------------------------------------------------
+struct Lds {
+  float* hin;  int ld_hin;   // [R][H+T]  h (cols 0..H-1) | time embedding (cols H..H+T-1)
+  float* hb;   int ld_hb;    // [R][H]    h after the per-block Dense (residual source)
+  float* P;    int ld_P;     // [R][2M]   per-node phi_e.0 halves; reused as phi_h ping-pong
+  float* macc; int ld_m;     // [R][M]    message aggregate
+  float* xc;                 // [R][D]    centred positions, updated per block
+  float* xc0;                // [R][D]    initial centred positions
+  float* dxacc;              // [R][D]    shift aggregate
+  float* mean;               // [2][MPW][D] input mean (primal, tangent)
+  float* temb;               // [MPW][T]
+  int*   feat;               // [MPW][N]
+  float* tail;               // first free float (solver state follows)
+};
+
+__host__ __device__ inline int align4(int n) { return (n + 3) & ~3; }
+
+template <int NT>
+__host__ __device__ inline int lds_eval_floats(int N, int D, int H, int T, int M, int MPW, int RP) {
+  const int R = RP * (1 + NT);
+  int n = 0;
+  n += align4(R * (H + T + 1));
+  n += align4(R * (H + 1));
+  n += align4(R * (2 * M + 3));
+  n += align4(R * (M + 1));
+  n += 3 * align4(R * D);
+  n += align4(2 * MPW * D);
+  n += align4(MPW * T);
+  n += align4(MPW * N);
+  return n;
+}
+
+template <int NT>
+__device__ inline Lds carve_lds(const Net& net, float* base) {
+  Lds s;
+  const int R = net.RP * (1 + NT);
+  float* p = base;
+  s.hin = p;  s.ld_hin = net.H + net.T + 1; p += align4(R * s.ld_hin);
+  s.hb = p;   s.ld_hb = net.H + 1;          p += align4(R * s.ld_hb);
+  s.P = p;    s.ld_P = 2 * net.M + 3;       p += align4(R * s.ld_P);
+  s.macc = p; s.ld_m = net.M + 1;           p += align4(R * s.ld_m);
+  s.xc = p;    p += align4(R * net.D);
+  s.xc0 = p;   p += align4(R * net.D);
+  s.dxacc = p; p += align4(R * net.D);
+  s.mean = p;  p += align4(2 * net.MPW * net.D);
+  s.temb = p;  p += align4(net.MPW * net.T);
+  s.feat = reinterpret_cast<int*>(p); p += align4(net.MPW * net.N);
+  s.tail = p;
+  return s;
+}
+
+// ---------------------------------------------------------------------------------------------------
+// scalar helpers
+// ---------------------------------------------------------------------------------------------------
+__device__ __forceinline__ float sigmoidf_(float x) {
+  return __builtin_amdgcn_rcpf(1.0f + __expf(-x));
+}
+
+// y = silu(p); dy = silu'(p) * dp
+template <int NT>
+__device__ __forceinline__ void silu_dual(float p, float dp, float& y, float& dy) {
+  const float s = sigmoidf_(p);
+  y = p * s;
+  if constexpr (NT) dy = s * (1.0f + p * (1.0f - s)) * dp;
+}
+
+// Returns `p` as a wave-uniform (SGPR) value the optimiser cannot see through: keeps per-tile weight loads inside
+// the tile loop (no LICM of a layer's weights into registers) and their addresses scalar.
+__device__ __forceinline__ const float* launder_uniform(const float* p) {
+  const uint64_t v = reinterpret_cast<uint64_t>(p);
+  uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  asm volatile("" : "+s"(lo), "+s"(hi));
+  return reinterpret_cast<const float*>(((uint64_t)hi << 32) | lo);
+}
+
+__device__ __forceinline__ f32x16 mfma32(float a, float b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+// accumulator row of register r for lane half kk (C/D map of the 32x32 f32 MFMA)
+__device__ __forceinline__ int acc_row(int r, int kk) { return (r & 3) + 8 * (r >> 2) + 4 * kk; }
+
+__device__ __forceinline__ void init_bias(f32x16& acc, const float* __restrict__ bias, int jb, int kk) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    f32x4 b = bias ? *reinterpret_cast<const f32x4*>(bias + jb * 32 + 8 * q + 4 * kk) : f32x4{0.f, 0.f, 0.f, 0.f};
+    acc[4 * q + 0] = b[0];
+    acc[4 * q + 1] = b[1];
+    acc[4 * q + 2] = b[2];
+    acc[4 * q + 3] = b[3];
+  }
+}
+
+// ---------------------------------------------------------------------------------------------------
+// node GEMM: Y[n][0:NOUT] = act([X1 | X2][n] W + b) (+ resid[n]); tangent rows RP+n share the A fragments
+// and get no bias, act'(pre) * (X_T W).
+// ---------------------------------------------------------------------------------------------------
+template <int NT>
+__device__ __forceinline__ void node_gemm(const float* X1, int ldx1, int K1, const float* X2, int ldx2, int K2,
+                                          const float* __restrict__ W, int ldw, const float* __restrict__ bias,
+                                          int NOUT, bool act, const float* resid, int ldr, float* Y, int ldy,
+                                          int RP, int nvalid, int wave, int lane) {
+  const int kk = lane >> 5, li = lane & 31;
+  const int njb = NOUT >> 5, nct = RP >> 5;
+  for (int task = wave; task < njb * nct; task += kWaves) {
+    const int jb = task % njb, ct = task / njb;
+    const int n = ct * 32 + li;
+    f32x16 acc, accT;
+    init_bias(acc, bias, jb, kk);
+    if constexpr (NT) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) accT[r] = 0.f;
+    }
+    const float* wcol = W + kk * ldw + jb * 32 + li;
+    {
+      const float* xr = X1 + n * ldx1 + kk;
+      const float* xrT = X1 + (RP + n) * ldx1 + kk;
+#pragma unroll 4
+      for (int k = 0; k < K1; k += 2) {
+        const float a = wcol[k * ldw];
+        acc = mfma32(a, xr[k], acc);
+        if constexpr (NT) accT = mfma32(a, xrT[k], accT);
+      }
+    }
+    if (K2 > 0) {
+      const float* w2 = wcol + K1 * ldw;
+      const float* xr = X2 + n * ldx2 + kk;
+      const float* xrT = X2 + (RP + n) * ldx2 + kk;
+#pragma unroll 4
+      for (int k = 0; k < K2; k += 2) {
+        const float a = w2[k * ldw];
+        acc = mfma32(a, xr[k], acc);
+        if constexpr (NT) accT = mfma32(a, xrT[k], accT);
+      }
+    }
+    if (n < nvalid) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int j = jb * 32 + acc_row(r, kk);
+        float y = acc[r], yT = 0.f;
+        if (act) {
+          silu_dual<NT>(acc[r], NT ? accT[r] : 0.f, y, yT);
+        } else if constexpr (NT) {
+          yT = accT[r];
+        }
+        if (resid) {
+          y += resid[n * ldr + j];
+          if constexpr (NT) yT += resid[(RP + n) * ldr + j];
+        }
+        Y[n * ldy + j] = y;
+        if constexpr (NT) Y[(RP + n) * ldy + j] = yT;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------------
+// edge-MLP chain layer: b = silu(a W + bias), all in registers (a, b: NF blocks of 32 rows x 32 edges)
+// ---------------------------------------------------------------------------------------------------
+template <int NF, int NT>
+__device__ __forceinline__ void chain_layer(const f32x16 (&a)[NF], const f32x16 (&aT)[NF], f32x16 (&b)[NF],
+                                            f32x16 (&bT)[NF], const float* __restrict__ Wpk,
+                                            const float* __restrict__ bias, int lane) {
+  const int kk = lane >> 5;
+#pragma unroll
+  for (int jb = 0; jb < NF; ++jb) {
+    f32x16 acc, accT;
+    init_bias(acc, bias, jb, kk);
+    if constexpr (NT) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) accT[r] = 0.f;
+    }
+    const f32x4* wp = reinterpret_cast<const f32x4*>(Wpk) + (jb * NF * 4) * 64 + lane;
+#pragma unroll
+    for (int fb = 0; fb < NF; ++fb) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f32x4 w = wp[(fb * 4 + q) * 64];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          acc = mfma32(w[e], a[fb][4 * q + e], acc);
+          if constexpr (NT) accT = mfma32(w[e], aT[fb][4 * q + e], accT);
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      float y, yT = 0.f;
+      silu_dual<NT>(acc[r], NT ? accT[r] : 0.f, y, yT);
+      b[jb][r] = y;
+      if constexpr (NT) bT[jb][r] = yT;
+    }
+  }
+}
+
+template <int NF, int NT, int NL>
+struct Chain {
+  // runs NL layers starting from `a`; the result ends in `a` if NL is even, else in `b`
+  __device__ __forceinline__ static void run(f32x16 (&a)[NF], f32x16 (&aT)[NF], f32x16 (&b)[NF], f32x16 (&bT)[NF],
+                                             const float* Wpk, const float* bias, int lane) {
+    chain_layer<NF, NT>(a, aT, b, bT, Wpk, bias, lane);
+    Chain<NF, NT, NL - 1>::run(b, bT, a, aT, Wpk + NF * NF * 1024, bias + NF * 32, lane);
+  }
+};
+template <int NF, int NT>
+struct Chain<NF, NT, 0> {
+  __device__ __forceinline__ static void run(f32x16 (&)[NF], f32x16 (&)[NF], f32x16 (&)[NF], f32x16 (&)[NF],
+                                             const float*, const float*, int) {}
+};
+
+// segmented (by receiver row) suffix sum over the 32 edge lanes of a half-wave
+struct SegScan {
+  bool ok[5];
+  bool head;
+  __device__ __forceinline__ void init(int seg, int li) {
+#pragma unroll
+    for (int o = 0; o < 5; ++o) {
+      const int off = 1 << o;
+      const int other = __shfl_down(seg, off, 32);
+      ok[o] = (li + off < 32) && (other == seg);
+    }
+    const int prev = __shfl_up(seg, 1, 32);
+    head = (li == 0) || (prev != seg);
+  }
+  __device__ __forceinline__ float sum(float v) const {
+#pragma unroll
+    for (int o = 0; o < 5; ++o) {
+      const float w = __shfl_down(v, 1 << o, 32);
+      v = ok[o] ? v + w : v;
+    }
+    return v;
+  }
+};
+
+__device__ __forceinline__ void lds_add(float* p, float v) {
+  __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// phi_x output Dense(1) (egnn.py:83-85), shifts_ij = phi_x * r_ij / (C + |r_ij|) and their segment sum
+// (egnn.py:87-94)
+template <int NF, int NT, int D>
+__device__ __forceinline__ void edge_shift(const Net& net, const BlockW& bw, const Lds& s, const f32x16 (&px)[NF],
+                                           const f32x16 (&pxT)[NF], bool writer, const SegScan& sc, int rr,
+                                           const float (&r)[D], const float (&dr)[D], float length, float dlength,
+                                           int lane) {
+  const int kk = lane >> 5;
+  float phx = 0.f, phxT = 0.f;
+#pragma unroll
+  for (int fb = 0; fb < NF; ++fb)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const f32x4 w = *reinterpret_cast<const f32x4*>(bw.wx + fb * 32 + 8 * q + 4 * kk);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        phx += w[e] * px[fb][4 * q + e];
+        if constexpr (NT) phxT += w[e] * pxT[fb][4 * q + e];
+      }
+    }
+  phx += __shfl_xor(phx, 32);
+  if constexpr (NT) phxT += __shfl_xor(phxT, 32);
+  phx += bw.bx;
+  const float den = net.C + length;
+  const int RP = net.RP;
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    const float sh = sc.sum((phx * r[d]) / den);
+    if (writer && kk == 0) lds_add(&s.dxacc[rr * D + d], sh);
+    if constexpr (NT) {
+      const float shT = sc.sum((phxT * r[d] + phx * dr[d]) / den - (phx * r[d]) * dlength / (den * den));
+      if (writer && kk == 0) lds_add(&s.dxacc[(RP + rr) * D + d], shT);
+    }
+  }
+}
+
+// gate, message aggregation, phi_x torso + output, shifts (egnn.py:81-104); `m` holds the messages
+template <int NF, int NT, int L, int D>
+__device__ __forceinline__ void edge_tail(const Net& net, const BlockW& bw, const Lds& s, f32x16 (&m)[NF],
+                                          f32x16 (&mT)[NF], f32x16 (&o)[NF], f32x16 (&oT)[NF], bool valid,
+                                          int rr, const float (&r)[D], const float (&dr)[D], float length,
+                                          float dlength, int lane) {
+  const int kk = lane >> 5, li = lane & 31;
+  // gate e_ij = sigmoid(m_ij . w_g + b_g)  (egnn.py:99-101)
+  float part = 0.f, partT = 0.f;
+#pragma unroll
+  for (int fb = 0; fb < NF; ++fb)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const f32x4 w = *reinterpret_cast<const f32x4*>(bw.wg + fb * 32 + 8 * q + 4 * kk);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        part += w[e] * m[fb][4 * q + e];
+        if constexpr (NT) partT += w[e] * mT[fb][4 * q + e];
+      }
+    }
+  part += __shfl_xor(part, 32);
+  if constexpr (NT) partT += __shfl_xor(partT, 32);
+  const float g = sigmoidf_(part + bw.bg);
+  const float gT = NT ? g * (1.0f - g) * partT : 0.f;
+
+  // m_i = scatter_sum(m_ij * e_ij) (the / sqrt(N-1) happens in the node update)   (egnn.py:102-104)
+  SegScan sc;
+  sc.init(valid ? rr : -1, li);
+  const bool writer = valid && sc.head;
+  const int RP = net.RP;
+#pragma unroll
+  for (int fb = 0; fb < NF; ++fb)
+#pragma unroll
+    for (int r16 = 0; r16 < 16; ++r16) {
+      const int row = fb * 32 + acc_row(r16, kk);
+      const float v = sc.sum(m[fb][r16] * g);
+      if (writer) lds_add(&s.macc[rr * s.ld_m + row], v);
+      if constexpr (NT) {
+        const float vT = sc.sum(gT * m[fb][r16] + g * mT[fb][r16]);
+        if (writer) lds_add(&s.macc[(RP + rr) * s.ld_m + row], vT);
+      }
+    }
+
+  // phi_x torso (egnn.py:82) then its Dense(1) and the shifts
+  const float* We = bw.We + (L - 1) * NF * NF * 1024;
+  const float* be = bw.be + (L - 1) * NF * 32;
+  We = launder_uniform(We);
+  Chain<NF, NT, L>::run(m, mT, o, oT, We, be, lane);
+  if constexpr (L % 2 == 0) {
+    edge_shift<NF, NT, D>(net, bw, s, m, mT, writer, sc, rr, r, dr, length, dlength, lane);
+  } else {
+    edge_shift<NF, NT, D>(net, bw, s, o, oT, writer, sc, rr, r, dr, length, dlength, lane);
+  }
+}
+
+// one 32-edge tile through phi_e / gate / phi_x  (egnn.py:72-95)
+template <int NF, int NT, int L, int D>
+__device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, const Lds& s, int tile, int lane) {
+  const int kk = lane >> 5, li = lane & 31;
+  const int N = net.N, E = net.E, nn1 = N - 1, RP = net.RP, M = NF * 32;
+  // each molecule owns EP = 32*ceil(E/32) edge slots, so its tiles (and every rounding inside them) do not
+  // depend on which slot of the workgroup, i.e. which batch position, it occupies
+  const int mol = (tile * 32) / net.EP;
+  const int e_in = tile * 32 + li - mol * net.EP;
+  const bool valid = (mol < net.MPW) && (e_in < E);
+  const int el = valid ? e_in : 0;
+  const int i = el / nn1;
+  const int jj = el - i * nn1;
+  int sd = i + 1 + jj;
+  if (sd >= N) sd -= N;
+  const int rr = mol * N + i, rs = mol * N + sd;   // receiver / sender rows (graph.py:10-13)
+
+  // r_ij = x_i - x_j, lengths = safe_norm (egnn.py:73-74, numerical.py:7-10)
+  float r[D], dr[D];
+  float x2 = 0.f;
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    r[d] = s.xc[rr * D + d] - s.xc[rs * D + d];
+    x2 += r[d] * r[d];
+  }
+  const bool zero = (x2 == 0.f);
+  const float length = sqrtf(zero ? 1.0f : x2);
+  const float len2 = length * length;
+  float dlength = 0.f, dlen2 = 0.f;
+  if constexpr (NT) {
+    float rdr = 0.f;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      dr[d] = s.xc[(RP + rr) * D + d] - s.xc[(RP + rs) * D + d];
+      rdr += r[d] * dr[d];
+    }
+    dlength = zero ? 0.f : rdr / length;
+    dlen2 = 2.0f * length * dlength;
+  } else {
+#pragma unroll
+    for (int d = 0; d < D; ++d) dr[d] = 0.f;
+  }
+
+  // phi_e layer 1 from the per-node halves: pre = P_s[s] + P_r[r] + |r|^2 w_d  (egnn.py:76,79)
+  f32x16 X0[NF], X1[NF], T0[NF], T1[NF];
+  const float* Ps = s.P + rs * s.ld_P;
+  const float* Pr = s.P + rr * s.ld_P + M;
+  const float* PsT = s.P + (RP + rs) * s.ld_P;
+  const float* PrT = s.P + (RP + rr) * s.ld_P + M;
+#pragma unroll
+  for (int fb = 0; fb < NF; ++fb)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const f32x4 w = *reinterpret_cast<const f32x4*>(bw.wd + fb * 32 + 8 * q + 4 * kk);
+#pragma unroll
+      for (int e4 = 0; e4 < 4; ++e4) {
+        const int row = fb * 32 + 8 * q + 4 * kk + e4;
+        const float p = Ps[row] + Pr[row] + len2 * w[e4];
+        float y, yT = 0.f;
+        if constexpr (NT) {
+          const float pT = PsT[row] + PrT[row] + dlen2 * w[e4];
+          silu_dual<NT>(p, pT, y, yT);
+          T0[fb][4 * q + e4] = yT;
+        } else {
+          silu_dual<NT>(p, 0.f, y, yT);
+        }
+        X0[fb][4 * q + e4] = y;
+      }
+    }
+  // phi_e layers 2..L.  The weight pointer is laundered through an empty asm so the (tile-invariant) weight
+  // loads are not hoisted out of the tile loop into thousands of live registers.
+  const float* We = launder_uniform(bw.We);
+  Chain<NF, NT, L - 1>::run(X0, T0, X1, T1, We, bw.be, lane);
+  if constexpr ((L - 1) % 2 == 0) {
+    edge_tail<NF, NT, L, D>(net, bw, s, X0, T0, X1, T1, valid, rr, r, dr, length, dlength, lane);
+  } else {
+    edge_tail<NF, NT, L, D>(net, bw, s, X1, T1, X0, T0, valid, rr, r, dr, length, dlength, lane);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------------
+// one full evaluation.  x_in/tan_in/v_out/tan_out: LDS [MPW][N*D]; t_in: LDS [MPW] (actual time).
+// Must be called by all 256 threads; returns after a barrier.
+// ---------------------------------------------------------------------------------------------------
+template <int NF, int NT, int L, int D>
+__device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const float* x_in, const float* t_in, const float* tan_in,
+                          float* v_out, float* tan_out) {
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int N = net.N, H = net.H, T = net.T, M = NF * 32, RP = net.RP, MPW = net.MPW, ND = net.ND;
+  const int nvalid = MPW * N;
+  const int R = RP * (1 + NT);
+
+  // ---- prologue: input mean, centring (egnn.py:160), embedding (build_cnf.py:79-83) ----
+  for (int idx = tid; idx < MPW * D * (1 + NT); idx += kThreads) {
+    const int which = idx / (MPW * D), md = idx - which * MPW * D, m = md / D, d = md - m * D;
+    const float* src = (which == 0 ? x_in : tan_in) + m * ND + d;
+    float acc = 0.f;
+    for (int i = 0; i < N; ++i) acc += src[i * D];
+    s.mean[idx] = acc / (float)N;
+  }
+  for (int idx = tid; idx < MPW * T; idx += kThreads) {
+    const int m = idx / T, k = idx - m * T, half = T >> 1;
+    const float ts = t_in[m] * 1000.0f;                   // build_cnf.py:23
+    const float arg = ts * net.freqs[k < half ? k : k - half];
+    s.temb[idx] = k < half ? sinf(arg) : cosf(arg);
+  }
+  __syncthreads();
+  for (int idx = tid; idx < nvalid * D * (1 + NT); idx += kThreads) {
+    const int which = idx / (nvalid * D), nd = idx - which * nvalid * D, n = nd / D, d = nd - n * D;
+    const int m = n / N;
+    const float* src = which == 0 ? x_in : tan_in;
+    const float v = src[m * ND + (n - m * N) * D + d] - s.mean[which * MPW * D + m * D + d];
+    const int row = which * RP + n;
+    s.xc[row * D + d] = v;
+    s.xc0[row * D + d] = v;
+  }
+  for (int idx = tid; idx < R * (H + T); idx += kThreads) {
+    const int row = idx / (H + T), c = idx - row * (H + T);
+    float v = 0.f;
+    if (row < nvalid) {
+      const int m = row / N;
+      v = c < H ? net.emb[s.feat[row] * H + c] : s.temb[m * T + (c - H)];
+    }
+    s.hin[row * s.ld_hin + c] = v;
+  }
+  __syncthreads();
+
+  const int ntiles = (MPW * net.EP) >> 5;
+  for (int k = 0; k < net.K; ++k) {
+    const BlockW& bw = net.blk[k];
+    // h <- Dense([h | temb])  (egnn.py:166-167)
+    node_gemm<NT>(s.hin, s.ld_hin, H + T, nullptr, 0, 0, bw.Wn, H, bw.bn, H, false, nullptr, 0, s.hb, s.ld_hb, RP,
+                  nvalid, wave, lane);
+    __syncthreads();
+    // per-node halves of phi_e layer 1
+    node_gemm<NT>(s.hb, s.ld_hb, H, nullptr, 0, 0, bw.Wp, 2 * M, bw.bp, 2 * M, false, nullptr, 0, s.P, s.ld_P, RP,
+                  nvalid, wave, lane);
+    __syncthreads();
+    // edges
+    for (int tile = wave; tile < ntiles; tile += kWaves) edge_tile<NF, NT, L, D>(net, bw, s, tile, lane);
+    __syncthreads();
+    // node update: x += shift_i / (N-1) (egnn.py:95,113); m_i /= sqrt(N-1) (egnn.py:104)
+    for (int idx = tid; idx < R * D; idx += kThreads) {
+      s.xc[idx] += s.dxacc[idx] / net.nn1;
+      s.dxacc[idx] = 0.f;
+    }
+    for (int idx = tid; idx < R * M; idx += kThreads) {
+      const int row = idx / M, c = idx - row * M;
+      s.macc[row * s.ld_m + c] /= net.sqrt_nn1;
+    }
+    __syncthreads();
+    // phi_h = MLP((M,)*L + (H,)) on [m_i | h], residual (egnn.py:105-111)
+    float* Q0 = s.P;
+    float* Q1 = s.P + (M + 1);
+    node_gemm<NT>(s.macc, s.ld_m, M, s.hb, s.ld_hb, H, bw.Wh[0], M, bw.bh[0], M, true, nullptr, 0, Q0, s.ld_P, RP,
+                  nvalid, wave, lane);
+    __syncthreads();
+    for (int idx = tid; idx < R * M; idx += kThreads) {
+      const int row = idx / M, c = idx - row * M;
+      s.macc[row * s.ld_m + c] = 0.f;
+    }
+    for (int l = 1; l < L; ++l) {
+      node_gemm<NT>(Q0, s.ld_P, M, nullptr, 0, 0, bw.Wh[l], M, bw.bh[l], M, true, nullptr, 0, Q1, s.ld_P, RP,
+                    nvalid, wave, lane);
+      __syncthreads();
+      float* tq = Q0; Q0 = Q1; Q1 = tq;
+    }
+    node_gemm<NT>(Q0, s.ld_P, M, nullptr, 0, 0, bw.Wh[L], H, bw.bh[L], H, false, s.hb, s.ld_hb, s.hin, s.ld_hin, RP,
+                  nvalid, wave, lane);
+    __syncthreads();
+  }
+
+  // ---- epilogue: v = ((x_K - x_c0) - mean(x_in)) * final_scaling  (egnn.py:183-188) ----
+  for (int idx = tid; idx < nvalid * D * (1 + NT); idx += kThreads) {
+    const int which = idx / (nvalid * D), nd = idx - which * nvalid * D, n = nd / D, d = nd - n * D;
+    const int m = n / N;
+    const int row = which * RP + n;
+    const float v = ((s.xc[row * D + d] - s.xc0[row * D + d]) - s.mean[which * MPW * D + m * D + d]) * net.fs;
+    float* dst = which == 0 ? v_out : tan_out;
+    dst[m * ND + (n - m * N) * D + d] = v;
+  }
+  __syncthreads();
+}
+
+}  // namespace ecnf

@@ -1,0 +1,107 @@
+"""ctypes binding of libecnf_hip.so (C-ABI declared in include/ecnf.h).
+
+The library is built in-tree by ``__graft_entry__.build()`` (hipcc --offload-arch=gfx950) next to this file.
+There is no fallback: if the library is missing or fails to load, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional
+
+LIB_NAME = "libecnf_hip.so"
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+
+ECNF_OK, ECNF_E_INVALID, ECNF_E_UNSUPPORTED, ECNF_E_HIP, ECNF_E_MAX_STEPS = 0, 1, 2, 3, 4
+SOLVER_EULER, SOLVER_DOPRI5 = 0, 1
+DIV_NONE, DIV_HUTCHINSON, DIV_EXACT = 0, 1, 2
+
+# every symbol include/ecnf.h declares
+EXPORTED_SYMBOLS = (
+    "ecnf_abi_version", "ecnf_last_error", "ecnf_param_count", "ecnf_create", "ecnf_destroy",
+    "ecnf_vector_field", "ecnf_vf_jvp", "ecnf_integrate", "ecnf_base_sample", "ecnf_base_log_prob",
+    "ecnf_molecules_per_workgroup",
+)
+
+
+class EcnfCfg(ctypes.Structure):
+    _fields_ = [
+        ("n_nodes", ctypes.c_int32),
+        ("dim", ctypes.c_int32),
+        ("n_features", ctypes.c_int32),
+        ("hidden", ctypes.c_int32),
+        ("time_embedding_dim", ctypes.c_int32),
+        ("mlp_width", ctypes.c_int32),
+        ("mlp_depth", ctypes.c_int32),
+        ("n_blocks", ctypes.c_int32),
+        ("base_scale", ctypes.c_float),
+        ("normalization_constant", ctypes.c_float),
+    ]
+
+
+class EcnfSolveOpts(ctypes.Structure):
+    _fields_ = [
+        ("solver", ctypes.c_int32),
+        ("divergence", ctypes.c_int32),
+        ("t0", ctypes.c_float),
+        ("t1", ctypes.c_float),
+        ("dt0", ctypes.c_float),
+        ("rtol", ctypes.c_float),
+        ("atol", ctypes.c_float),
+        ("dtmin", ctypes.c_float),
+        ("max_steps", ctypes.c_int32),
+    ]
+
+
+class EcnfError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"ecnf error {code}: {msg}")
+        self.code = code
+
+
+class EcnfInvalid(EcnfError, ValueError):
+    pass
+
+
+_lib: Optional[ctypes.CDLL] = None
+
+
+def load(path: Optional[str] = None) -> ctypes.CDLL:
+    """Load (once) and type the C-ABI.  Raises FileNotFoundError / OSError when the HIP library is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = path or os.environ.get("ECNF_LIB", LIB_PATH)
+    if not os.path.exists(path):
+        raise FileNotFoundError(
+            f"{path} not found: build the HIP library first (python -c 'import __graft_entry__ as g; g.build()')")
+    lib = ctypes.CDLL(path)
+    P, I32, SZ = ctypes.c_void_p, ctypes.c_int32, ctypes.c_size_t
+    sig = {
+        "ecnf_abi_version": ([], ctypes.c_int),
+        "ecnf_last_error": ([], ctypes.c_char_p),
+        "ecnf_param_count": ([ctypes.POINTER(EcnfCfg), ctypes.POINTER(SZ)], ctypes.c_int),
+        "ecnf_create": ([ctypes.POINTER(EcnfCfg), P, SZ, ctypes.c_int, ctypes.POINTER(P)], ctypes.c_int),
+        "ecnf_destroy": ([P], ctypes.c_int),
+        "ecnf_vector_field": ([P, P, P, P, P, I32, P], ctypes.c_int),
+        "ecnf_vf_jvp": ([P, P, P, P, P, I32, P, P, I32, P], ctypes.c_int),
+        "ecnf_integrate": ([P, ctypes.POINTER(EcnfSolveOpts), P, P, P, P, P, P, P, I32, P], ctypes.c_int),
+        "ecnf_base_sample": ([P, P, P, I32, P], ctypes.c_int),
+        "ecnf_base_log_prob": ([P, P, P, I32, P], ctypes.c_int),
+        "ecnf_molecules_per_workgroup": ([P, I32, ctypes.POINTER(I32)], ctypes.c_int),
+    }
+    for name, (argtypes, restype) in sig.items():
+        fn = getattr(lib, name)
+        fn.argtypes = argtypes
+        fn.restype = restype
+    _lib = lib
+    return lib
+
+
+def check(rc: int) -> None:
+    if rc == ECNF_OK:
+        return
+    msg = load().ecnf_last_error().decode(errors="replace")
+    if rc in (ECNF_E_INVALID, ECNF_E_UNSUPPORTED):
+        raise EcnfInvalid(rc, msg)
+    raise EcnfError(rc, msg)

@@ -1,0 +1,130 @@
+/*
+ * ecnf.h — C-ABI of libecnf_hip.so, the MI355X (gfx950) equivariant-CNF sample / log_prob path.
+ *
+ * The reference (Kalyan0821/ecnf-baseline-neurips-2023) is pure JAX; its "plugin/operator API" for this
+ * path is the FlowMatchingCNF bundle and the three solver entry points.  Each function below replaces one
+ * of them (file:line in the reference snapshot):
+ *
+ *   ecnf_create / ecnf_destroy   <- build_cnf(...) + cnf.init params   ecnf/cnf/build_cnf.py:34-102
+ *                                   (the handle owns the device copy of the flat params blob)
+ *   ecnf_vector_field            <- cnf.apply(params, x, t, features)  ecnf/cnf/core.py:7-19,45;
+ *                                   FlatEgnn.__call__ build_cnf.py:68-93; EGNN egnn.py:130-190
+ *   ecnf_vf_jvp                  <- jax.vjp(cnf.apply) + vmap(vjp_fn)  ecnf/cnf/sample_and_log_prob.py:64-66,75-77
+ *                                   (forward-mode tangents J @ u instead of reverse-mode u^T J)
+ *   ecnf_integrate               <- diffrax.diffeqsolve(ODETerm, Dopri5, [PIDController])
+ *                                   sample_and_log_prob.py:28-38 (sample_cnf), :81-94 (get_log_prob),
+ *                                   :135-149 (sample_and_log_prob_cnf)
+ *   ecnf_base_sample             <- cnf.sample_base (distrax Transformed._sample_n)
+ *                                   zero_com_base.py:16-19,88-93 + build_cnf.py:46-61
+ *   ecnf_base_log_prob           <- cnf.log_prob_base  zero_com_base.py:21-24,64-84 + build_cnf.py:50-57
+ *   ecnf_last_error              <- the chex / diffrax exceptions (trace-time asserts, max_steps)
+ *
+ * Conventions
+ *   - every array argument is a DEVICE pointer (hipMalloc'd or a torch tensor's data_ptr()), fp32 / int32,
+ *     contiguous row-major; x is flat [batch, n_nodes*dim] exactly like the reference's flat events.
+ *   - `stream` is a hipStream_t (NULL = default stream).  Calls are stream-ordered and asynchronous,
+ *     except ecnf_create/ecnf_destroy which synchronise.
+ *   - return value: ECNF_OK or an ECNF_E_* code; ecnf_last_error() gives a thread-local message.
+ *   - one handle per device; a handle is not re-entrant, distinct handles may be used from distinct threads.
+ */
+#ifndef ECNF_H_
+#define ECNF_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ECNF_ABI_VERSION 1
+
+enum ecnf_status {
+  ECNF_OK = 0,
+  ECNF_E_INVALID = 1,      /* bad argument / shape (the reference's chex.assert_* failures) */
+  ECNF_E_UNSUPPORTED = 2,  /* a configuration this build has no kernel for */
+  ECNF_E_HIP = 3,          /* a HIP runtime error (message in ecnf_last_error) */
+  ECNF_E_MAX_STEPS = 4     /* reported per molecule through ecnf_integrate's `status` output */
+};
+
+enum ecnf_solver { ECNF_SOLVER_EULER = 0, ECNF_SOLVER_DOPRI5 = 1 };
+enum ecnf_divergence { ECNF_DIV_NONE = 0, ECNF_DIV_HUTCHINSON = 1, ECNF_DIV_EXACT = 2 };
+
+/* Model hyper-parameters: the `flow:` block of examples/config/{dw4,lj13,aldp,qm9}.yaml and the
+ * build_cnf(...) arguments (build_cnf.py:34-44).  mlp_units is (mlp_width,) * mlp_depth. */
+typedef struct ecnf_cfg {
+  int32_t n_nodes;             /* n_frames (N)                                   */
+  int32_t dim;                 /* spatial dim (D): 2 or 3                        */
+  int32_t n_features;          /* nn.Embed vocabulary                            */
+  int32_t hidden;              /* n_invariant_feat_hidden (H): multiple of 32    */
+  int32_t time_embedding_dim;  /* T: even, 4 <= T <= 16                          */
+  int32_t mlp_width;           /* M: 64, 128 or 256                              */
+  int32_t mlp_depth;           /* L = len(mlp_units): 2..4                       */
+  int32_t n_blocks;            /* n_blocks_egnn (K): 1..10                       */
+  float base_scale;            /* ScalarAffine scale of the base (build_cnf.py:46) */
+  float normalization_constant;/* EGCL C (egnn.py:127), 1.0 in the reference     */
+} ecnf_cfg;
+
+/* Options of one ODE solve (diffeqsolve arguments).  t0 < t1 samples (0 -> 1); t0 > t1 is the
+ * density direction of get_log_prob (1 -> 0).  dt0 > 0 selects ConstantStepSize; dt0 <= 0 selects
+ * PIDController(rtol, atol, dtmin) with Hairer's initial step (dt0=None in the reference). */
+typedef struct ecnf_solve_opts {
+  int32_t solver;      /* ecnf_solver                       */
+  int32_t divergence;  /* ecnf_divergence: d logp / dt term */
+  float t0, t1;
+  float dt0;           /* > 0: fixed step; <= 0: adaptive   */
+  float rtol, atol, dtmin;
+  int32_t max_steps;   /* diffrax default 4096              */
+} ecnf_solve_opts;
+
+typedef struct ecnf_handle ecnf_handle;
+
+/* Number of fp32 params the flat blob must hold for `cfg` (the jax ravel_pytree order of the flax
+ * params tree: EGNN_0/{k}/{Dense_0,Dense_1,phi_e,phi_h,phi_x_torso}, EGNN_0/Dense_k, final_scaling,
+ * Embed_0/embedding, sorted keys, bias before kernel). */
+int ecnf_param_count(const ecnf_cfg* cfg, size_t* n_floats);
+
+/* Upload `params` (HOST pointer, n_floats fp32) to `device`, repack them into MFMA fragment order and
+ * return a handle.  Synchronous. */
+int ecnf_create(const ecnf_cfg* cfg, const float* params, size_t n_floats, int device, ecnf_handle** out);
+int ecnf_destroy(ecnf_handle* h);
+
+/* v[b] = apply(params, x[b], t[b], feat[b])   (x, v: [batch, N*D]; t: [batch]; feat: [batch, N]). */
+int ecnf_vector_field(ecnf_handle* h, const float* x, const float* t, const int32_t* feat, float* v,
+                      int32_t batch, void* stream);
+
+/* Forward-mode Jacobian-vector products: tan_out[b, k] = (d apply / d x)(x[b]) @ tan_in[b, k] for
+ * k < n_tangents (tan_in/tan_out: [batch, n_tangents, N*D]); v as in ecnf_vector_field (may be NULL). */
+int ecnf_vf_jvp(ecnf_handle* h, const float* x, const float* t, const int32_t* feat, const float* tan_in,
+                int32_t n_tangents, float* v, float* tan_out, int32_t batch, void* stream);
+
+/* Solve the ODE for every molecule of the batch in ONE launch (each workgroup integrates its molecules
+ * end to end; adaptive steps are per molecule, as under jax.vmap).
+ *   y0   [batch, N*D]  initial positions (at t0)
+ *   eps  [batch, N*D]  Hutchinson probe (required for ECNF_DIV_HUTCHINSON, else ignored / NULL)
+ *   y1   [batch, N*D]  positions at t1
+ *   dlogp[batch]       l(t1) with dl/dt = div v, l(t0) = 0 (NULL allowed when divergence == NONE)
+ *   nfe  [batch]       vector-field evaluations spent on the molecule (NULL allowed)
+ *   status [batch]     ECNF_OK or ECNF_E_MAX_STEPS per molecule (NULL allowed) */
+int ecnf_integrate(ecnf_handle* h, const ecnf_solve_opts* opts, const float* y0, const int32_t* feat,
+                   const float* eps, float* y1, float* dlogp, int32_t* nfe, int32_t* status, int32_t batch,
+                   void* stream);
+
+/* x0 = base_scale * (z - mean_nodes(z)) for a standard-normal draw z [batch, N*D]. */
+int ecnf_base_sample(ecnf_handle* h, const float* z, float* x0, int32_t batch, void* stream);
+
+/* log_prob_base(y) [batch] of the scaled zero-CoM Gaussian. */
+int ecnf_base_log_prob(ecnf_handle* h, const float* y, float* log_p, int32_t batch, void* stream);
+
+/* Molecules processed by one workgroup for this handle (diagnostic; kernels pick it from the LDS budget). */
+int ecnf_molecules_per_workgroup(ecnf_handle* h, int32_t with_tangent, int32_t* mpw);
+
+/* Thread-local description of the last error ("" when none). */
+const char* ecnf_last_error(void);
+
+int ecnf_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ECNF_H_ */

@@ -1,0 +1,239 @@
+"""GPU parity: libecnf_hip.so (through the C-ABI) against the CPU oracle on identical seeded inputs.
+
+Tolerances (fp32 kernel vs fp64 oracle; stated per test):
+  * one vector-field evaluation / JVP: max |err| <= 2e-5 * max(1, max |ref|)
+  * fixed-step trajectories (100 Euler steps, 20 Dopri5 steps): max |err| <= 1e-4
+  * adaptive Dopri5: step sequences may fork in fp32, so final states <= 2e-3 and NFE within 15 %
+  * log-densities: |err| <= 2e-3 absolute (values are O(10-100))
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import ecnf_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+if not torch.cuda.is_available():  # collected on CPU-only hosts, skipped there
+    pytest.skip("needs a ROCm GPU", allow_module_level=True)
+
+from ecnf_amd import CONFIGS, CNFConfig  # noqa: E402
+from ecnf_amd import _lib  # noqa: E402
+from ecnf_amd.engine import EcnfHandle, SolveOptions  # noqa: E402
+
+DEV = torch.device("cuda", 0)
+
+# a small config for the expensive exact-trace tests (same kernels as ALDP: M=64, L=2)
+TINY = CNFConfig(n_nodes=5, dim=3, n_features=2, hidden=32, mlp_width=64, mlp_depth=2, n_blocks=2,
+                 base_scale=0.5)
+
+
+def _ocfg(cfg: CNFConfig) -> O.CNFConfig:
+    return O.CNFConfig(n_nodes=cfg.n_nodes, dim=cfg.dim, n_features=cfg.n_features, hidden=cfg.hidden,
+                       time_embedding_dim=cfg.time_embedding_dim, mlp_width=cfg.mlp_width, mlp_depth=cfg.mlp_depth,
+                       n_blocks=cfg.n_blocks, base_scale=cfg.base_scale, sigma_min=cfg.sigma_min)
+
+
+_HANDLES = {}
+
+
+def setup(cfg, B, seed=0, stress=True):
+    oc = _ocfg(cfg)
+    params = O.init_params(oc, seed)
+    if stress:
+        params = O.stress_params(params, oc)
+    key = (cfg, seed, stress)
+    if key not in _HANDLES:
+        _HANDLES[key] = EcnfHandle(cfg, params, 0)
+    h = _HANDLES[key]
+    rng = np.random.default_rng(seed + 1)
+    z = rng.standard_normal((B, cfg.event_dim)).astype(np.float32)
+    x0 = O.base_sample(z, oc)
+    feat = rng.integers(0, cfg.n_features, (B, cfg.n_nodes)).astype(np.int32)
+    return oc, params, h, z, x0, feat
+
+
+def g(a, dtype=torch.float32):
+    return torch.as_tensor(np.asarray(a), device=DEV, dtype=dtype)
+
+
+def rel_err(got, ref):
+    got = got.detach().cpu().numpy() if torch.is_tensor(got) else got
+    return float(np.abs(got - ref).max() / max(1.0, np.abs(ref).max()))
+
+
+# ------------------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("name", ["dw4", "lj13", "aldp", "qm9"])
+def test_vector_field(name):
+    cfg = CONFIGS[name]
+    oc, params, h, z, x0, feat = setup(cfg, B=2 * 4 + 3)
+    B = x0.shape[0]
+    t = np.linspace(0.0, 1.0, B).astype(np.float32)
+    v = h.vector_field(g(x0), g(t), g(feat, torch.int32))
+    ref = O.egnn_vector_field(params, oc, x0, t, feat, dtype=np.float64)
+    assert rel_err(v, ref) <= 2e-5, rel_err(v, ref)
+
+
+@pytest.mark.parametrize("name", ["dw4", "lj13", "aldp"])
+def test_jvp(name):
+    cfg = CONFIGS[name]
+    oc, params, h, z, x0, feat = setup(cfg, B=5)
+    t = np.full(5, 0.37, np.float32)
+    u = np.random.default_rng(3).standard_normal((5, 3, cfg.event_dim)).astype(np.float32)
+    v, ju = h.jvp(g(x0), g(t), g(feat, torch.int32), g(u))
+    vr, jr = O.egnn_vector_field(params, oc, x0, t, feat, tangents=u, dtype=np.float64)
+    assert rel_err(v, vr) <= 2e-5
+    assert rel_err(ju, jr) <= 2e-5, rel_err(ju, jr)
+
+
+def test_batch_position_invariance():
+    """A molecule's output is bitwise independent of its batch slot (shards concatenate bit-identically)."""
+    cfg = CONFIGS["lj13"]
+    oc, params, h, z, x0, feat = setup(cfg, B=13)
+    t = np.linspace(0.1, 0.9, 13).astype(np.float32)
+    v_all = h.vector_field(g(x0), g(t), g(feat, torch.int32)).cpu().numpy()
+    for lo, hi in [(0, 1), (3, 4), (5, 13), (1, 7)]:
+        v_part = h.vector_field(g(x0[lo:hi]), g(t[lo:hi]), g(feat[lo:hi], torch.int32)).cpu().numpy()
+        assert np.array_equal(v_part, v_all[lo:hi])
+    y_all, _, _, _ = h.integrate(g(x0), g(feat, torch.int32), 0.0, 1.0, SolveOptions("euler", 0.1))
+    y_part, _, _, _ = h.integrate(g(x0[5:9]), g(feat[5:9], torch.int32), 0.0, 1.0, SolveOptions("euler", 0.1))
+    assert torch.equal(y_all[5:9], y_part)
+
+
+def test_equivariance_and_translation():
+    """KAT-2 (ecnf/nets/egnn_test.py:9-31, ecnf/utils/test.py:60-76) on the device, fp32 tolerance 2e-5."""
+    from scipy.spatial.transform import Rotation
+    cfg = CONFIGS["lj13"]
+    oc, params, h, z, x0, feat = setup(cfg, B=4)
+    t = np.full(4, 0.5, np.float32)
+    R = Rotation.random(random_state=7).as_matrix().astype(np.float32)
+    rot = lambda a: (a.reshape(-1, cfg.n_nodes, 3) @ R.T).reshape(a.shape[0], -1)
+    v = h.vector_field(g(x0), g(t), g(feat, torch.int32)).cpu().numpy()
+    vr = h.vector_field(g(rot(x0)), g(t), g(feat, torch.int32)).cpu().numpy()
+    assert np.abs(rot(v) - vr).max() <= 2e-5 * max(1, np.abs(v).max())
+    shift = np.tile(np.array([0.3, -1.2, 2.0], np.float32), cfg.n_nodes)[None]
+    vs = h.vector_field(g(x0 + shift), g(t), g(feat, torch.int32)).cpu().numpy()
+    assert np.abs(vs - v).max() <= 2e-5 * max(1, np.abs(v).max())
+
+
+def test_coincident_atoms_safe_norm():
+    """safe_norm returns 1 for zero-length edges (numerical.py:7-10): finite output matching the oracle."""
+    cfg = CONFIGS["lj13"]
+    oc, params, h, z, x0, feat = setup(cfg, B=3)
+    x0 = x0.copy()
+    x0[0, 3:6] = x0[0, 0:3]          # atoms 0 and 1 coincide
+    x0[1] = 0.0                      # every atom at the origin
+    t = np.array([0.2, 0.5, 0.8], np.float32)
+    v = h.vector_field(g(x0), g(t), g(feat, torch.int32))
+    assert torch.isfinite(v).all()
+    ref = O.egnn_vector_field(params, oc, x0, t, feat, dtype=np.float64)
+    assert rel_err(v, ref) <= 2e-5
+    u = np.random.default_rng(1).standard_normal((3, 2, cfg.event_dim)).astype(np.float32)
+    _, ju = h.jvp(g(x0), g(t), g(feat, torch.int32), g(u))
+    _, jr = O.egnn_vector_field(params, oc, x0, t, feat, tangents=u, dtype=np.float64)
+    assert rel_err(ju, jr) <= 2e-5
+
+
+# ------------------------------------------------------------------------------------------------------
+def test_base_distribution():
+    cfg = CONFIGS["aldp"]
+    oc, params, h, z, x0, feat = setup(cfg, B=9)
+    x = h.base_sample(g(z))
+    assert rel_err(x, O.base_sample(z, oc, np.float64)) <= 1e-6
+    lp = h.base_log_prob(g(x0))
+    assert np.abs(lp.cpu().numpy() - O.base_log_prob(x0, oc)).max() <= 1e-3
+
+
+@pytest.mark.parametrize("name", ["lj13", "dw4"])
+def test_euler_sample(name):
+    cfg = CONFIGS[name]
+    oc, params, h, z, x0, feat = setup(cfg, B=9)
+    y1, _, nfe, status = h.integrate(g(x0), g(feat, torch.int32), 0.0, 1.0, SolveOptions("euler", 0.01))
+    ref, nfe_ref = O.sample_cnf(params, oc, x0, feat, solver="euler", dt0=0.01, dtype=np.float64)
+    assert np.abs(y1.cpu().numpy() - ref).max() <= 1e-4
+    assert (nfe.cpu().numpy() == 100).all() and (nfe_ref == 100).all()
+    assert (status.cpu().numpy() == 0).all()
+
+
+def test_dopri5_fixed_sample():
+    cfg = CONFIGS["lj13"]
+    oc, params, h, z, x0, feat = setup(cfg, B=6)
+    y1, _, nfe, _ = h.integrate(g(x0), g(feat, torch.int32), 0.0, 1.0, SolveOptions("dopri5", 0.05))
+    ref, nfe_ref = O.sample_cnf(params, oc, x0, feat, solver="dopri5", dt0=0.05, dtype=np.float64)
+    assert np.abs(y1.cpu().numpy() - ref).max() <= 1e-4
+    assert (nfe.cpu().numpy() == 121).all() and (nfe_ref == 121).all()
+
+
+@pytest.mark.parametrize("name", ["dw4", "aldp"])
+def test_dopri5_adaptive_sample(name):
+    cfg = CONFIGS[name]
+    oc, params, h, z, x0, feat = setup(cfg, B=5)
+    y1, _, nfe, _ = h.integrate(g(x0), g(feat, torch.int32), 0.0, 1.0, SolveOptions("dopri5", None))
+    ref, nfe_ref = O.sample_cnf(params, oc, x0, feat, solver="dopri5", dt0=None, dtype=np.float32)
+    assert np.abs(y1.cpu().numpy() - ref).max() <= 2e-3
+    nfe = nfe.cpu().numpy()
+    assert np.all(np.abs(nfe - nfe_ref) <= 0.15 * nfe_ref + 7), (nfe, nfe_ref)
+
+
+def test_log_prob_exact_fixed():
+    """get_log_prob(approx=False, use_fixed_step_size=True): 1 -> 0 with the full N*D trace."""
+    cfg = TINY
+    oc, params, h, z, x0, feat = setup(cfg, B=5)
+    x, dl, nfe, _ = h.integrate(g(x0), g(feat, torch.int32), 1.0, 0.0, SolveOptions("dopri5", 0.05),
+                                divergence=_lib.DIV_EXACT)
+    lp_ref, lp0_ref, dl_ref, nfe_ref, x_ref = O.get_log_prob(params, oc, x0, feat, approx=False, solver="dopri5",
+                                                             dt0=0.05, dtype=np.float64)
+    assert np.abs(x.cpu().numpy() - x_ref).max() <= 1e-4
+    assert np.abs(dl.cpu().numpy() - dl_ref).max() <= 2e-3
+    lp = h.base_log_prob(x) + dl
+    assert np.abs(lp.cpu().numpy() - lp_ref).max() <= 2e-3
+
+
+def test_sample_and_log_prob_hutchinson_fixed():
+    """sample_and_log_prob_cnf(approx=True, fixed step): eps is the raw draw z behind x0 (reference quirk)."""
+    cfg = CONFIGS["lj13"]
+    oc, params, h, z, x0, feat = setup(cfg, B=4)
+    x1, dl, nfe, _ = h.integrate(g(x0), g(feat, torch.int32), 0.0, 1.0, SolveOptions("dopri5", 0.05),
+                                 divergence=_lib.DIV_HUTCHINSON, eps=g(z))
+    x1r, lq_ref, _ = O.sample_and_log_prob(params, oc, x0, feat, eps=z, approx=True, solver="dopri5", dt0=0.05,
+                                           dtype=np.float64)
+    assert np.abs(x1.cpu().numpy() - x1r).max() <= 1e-4
+    lq = (h.base_log_prob(g(x0)) - dl).cpu().numpy()
+    assert np.abs(lq - lq_ref).max() <= 2e-3
+
+
+def test_log_prob_adaptive_hutchinson():
+    cfg = CONFIGS["aldp"]
+    oc, params, h, z, x0, feat = setup(cfg, B=3)
+    eps = np.random.default_rng(4321).standard_normal(x0.shape).astype(np.float32)
+    x, dl, nfe, _ = h.integrate(g(x0), g(feat, torch.int32), 1.0, 0.0, SolveOptions("dopri5", None),
+                                divergence=_lib.DIV_HUTCHINSON, eps=g(eps))
+    lp_ref, lp0_ref, dl_ref, nfe_ref, x_ref = O.get_log_prob(params, oc, x0, feat, eps=eps, approx=True,
+                                                             solver="dopri5", dt0=None, dtype=np.float32)
+    assert np.abs(x.cpu().numpy() - x_ref).max() <= 2e-3
+    assert np.abs(dl.cpu().numpy() - dl_ref).max() <= 2e-2
+
+
+# ------------------------------------------------------------------------------------------------------
+def test_max_steps_reported():
+    cfg = CONFIGS["dw4"]
+    oc, params, h, z, x0, feat = setup(cfg, B=3)
+    with pytest.raises(RuntimeError, match="max_steps"):
+        h.integrate(g(x0), g(feat, torch.int32), 0.0, 1.0, SolveOptions("dopri5", None, max_steps=2))
+    _, _, _, status = h.integrate(g(x0), g(feat, torch.int32), 0.0, 1.0, SolveOptions("euler", 0.01, max_steps=10),
+                                  check_status=False)
+    assert (status.cpu().numpy() == _lib.ECNF_E_MAX_STEPS).all()
+
+
+def test_empty_batch_and_errors():
+    cfg = CONFIGS["lj13"]
+    oc, params, h, z, x0, feat = setup(cfg, B=2)
+    e = torch.empty(0, cfg.event_dim, device=DEV)
+    v = h.vector_field(e, torch.empty(0, device=DEV), torch.empty(0, cfg.n_nodes, device=DEV, dtype=torch.int32))
+    assert v.shape == (0, cfg.event_dim)
+    with pytest.raises(ValueError):
+        h.vector_field(g(x0[:, :-1]), g([0.1, 0.2]), g(feat, torch.int32))
+    with pytest.raises(ValueError):
+        h.integrate(g(x0), g(feat, torch.int32), 0.0, 1.0, SolveOptions("euler", None))
+    with pytest.raises(ValueError):
+        h.vector_field(g(x0), g([0.1, 0.2]), None)
