@@ -64,7 +64,7 @@ def main():
     ap.add_argument("--batch", type=int, default=1024, help="molecules per GPU per step")
     ap.add_argument("--config", default="lj13")
     ap.add_argument("--nfe", type=int, default=100)
-    ap.add_argument("--cpu-molecules", type=int, default=48, help="bounded CPU-baseline sample (0 = skip)")
+    ap.add_argument("--cpu-molecules", type=int, default=160, help="bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "0") or 0))
     args = ap.parse_args()
 

@@ -115,8 +115,11 @@ __device__ __forceinline__ void joint_field(const Net& net, const Lds& s, const 
   __syncthreads();
 }
 
-// rms over the (x, logp) leaves of one molecule: sqrt((sum_c a_c^2 + b^2) / (ND + 1))
-__device__ inline float rms_joint(float sumsq_x, float l, int ND) { return sqrtf((sumsq_x + l * l) / (float)(ND + 1)); }
+// diffrax rms_norm over the leaves of one molecule's state: (x, logp) when the divergence is tracked
+// (get_log_prob / sample_and_log_prob_cnf), x alone for sample_cnf (sample_and_log_prob.py:28-37 has y0 = x0)
+__device__ inline float rms_state(float sumsq_x, float l, int ND, bool track) {
+  return track ? sqrtf((sumsq_x + l * l) / (float)(ND + 1)) : sqrtf(sumsq_x / (float)ND);
+}
 
 enum Phase { kEuler = 0, kInit0 = 1, kInit1 = 2, kFsal = 3, kStage = 4 };
 
@@ -134,6 +137,7 @@ __global__ __launch_bounds__(kThreads) void integrate_kernel(Net net, SolveP sp,
   const int mol0 = blockIdx.x * MPW;
   const int nmol = min(MPW, B - mol0);
   const int a = align4(MPW * ND), b = align4(MPW);
+  const bool track = sp.div != ECNF_DIV_NONE;
 
   // zero the eval scratch (aggregates must start at +0; padding rows stay finite)
   for (int i = tid; i < (int)(s.tail - smem); i += kThreads) smem[i] = 0.f;
@@ -225,8 +229,8 @@ __global__ __launch_bounds__(kThreads) void integrate_kernel(Net net, SolveP sp,
           sf += (st.kx[tid * ND + c] / sc) * (st.kx[tid * ND + c] / sc);
         }
         const float scl = sp.atol + fabsf(st.lp[tid]) * sp.rtol;
-        const float d0 = rms_joint(sy, st.lp[tid] / scl, ND);
-        const float d1 = rms_joint(sf, st.kl[tid] / scl, ND);
+        const float d0 = rms_state(sy, st.lp[tid] / scl, ND, track);
+        const float d1 = rms_state(sf, st.kl[tid] / scl, ND, track);
         const bool cond = (d0 < 1e-5f) || (d1 < 1e-5f);
         const float d1s = cond ? 1.0f : d1;
         st.h0[tid] = cond ? 1e-6f : 0.01f * (d0 / d1s);
@@ -244,7 +248,7 @@ __global__ __launch_bounds__(kThreads) void integrate_kernel(Net net, SolveP sp,
         const float scl = sp.atol + fabsf(st.lp[tid]) * sp.rtol;
         const float h0 = st.h0[tid];
         const float d1 = st.l1[tid];
-        const float d2 = rms_joint(s2, (st.kl[b + tid] - st.kl[tid]) / scl, ND) / h0;
+        const float d2 = rms_state(s2, (st.kl[b + tid] - st.kl[tid]) / scl, ND, track) / h0;
         const float maxd = fmaxf(d1, d2);
         const float h1 = maxd <= 1e-15f ? fmaxf(1e-6f, h0 * 1e-3f) : powf(0.01f / maxd, 0.2f);
         const float dt = fminf(100.0f * h0, h1);
@@ -283,7 +287,7 @@ __global__ __launch_bounds__(kThreads) void integrate_kernel(Net net, SolveP sp,
           for (int j = 0; j < 7; ++j) el += kBerr[j] * st.kl[j * b + m];
           el = h * el;
           const float scl = sp.atol + fmaxf(fabsf(st.lp[m]), fabsf(l1)) * sp.rtol;
-          const float err = rms_joint(ssum, el / scl, ND);
+          const float err = rms_state(ssum, el / scl, ND, track);
           keep = (err < 1.0f) || st.atmin[m];
           const float inv = 1.0f / err;
           float factor = 0.9f * powf(inv, 0.2f);
@@ -792,9 +796,10 @@ int ecnf_molecules_per_workgroup(ecnf_handle* h, int32_t with_tangent, int32_t* 
 
 int ecnf_vector_field(ecnf_handle* h, const float* x, const float* t, const int32_t* feat, float* v, int32_t batch,
                       void* stream) {
-  if (!h || !x || !t || !feat || !v) return fail(ECNF_E_INVALID, "NULL argument");
+  if (!h) return fail(ECNF_E_INVALID, "NULL handle");
   if (batch < 0) return fail(ECNF_E_INVALID, "batch < 0");
   if (batch == 0) return ECNF_OK;
+  if (!x || !t || !feat || !v) return fail(ECNF_E_INVALID, "NULL argument");
   HIP_TRY(hipSetDevice(h->device));
   HIP_TRY(dispatch_vf(h, 0, x, t, feat, nullptr, 0, v, nullptr, batch, (hipStream_t)stream));
   g_err.clear();
@@ -803,8 +808,9 @@ int ecnf_vector_field(ecnf_handle* h, const float* x, const float* t, const int3
 
 int ecnf_vf_jvp(ecnf_handle* h, const float* x, const float* t, const int32_t* feat, const float* tan_in,
                 int32_t n_tangents, float* v, float* tan_out, int32_t batch, void* stream) {
-  if (!h || !x || !t || !feat || !tan_in || !tan_out) return fail(ECNF_E_INVALID, "NULL argument");
+  if (!h) return fail(ECNF_E_INVALID, "NULL handle");
   if (batch < 0 || n_tangents < 1) return fail(ECNF_E_INVALID, "batch < 0 or n_tangents < 1");
+  if (batch > 0 && (!x || !t || !feat || !tan_in || !tan_out)) return fail(ECNF_E_INVALID, "NULL argument");
   if (h->net[1].MPW == 0)
     return fail(ECNF_E_UNSUPPORTED, "no tangent kernel for mlp_width=" + std::to_string(h->cfg.mlp_width));
   if (batch == 0) return ECNF_OK;
@@ -816,12 +822,15 @@ int ecnf_vf_jvp(ecnf_handle* h, const float* x, const float* t, const int32_t* f
 
 int ecnf_integrate(ecnf_handle* h, const ecnf_solve_opts* o, const float* y0, const int32_t* feat, const float* eps,
                    float* y1, float* dlogp, int32_t* nfe, int32_t* status, int32_t batch, void* stream) {
-  if (!h || !o || !y0 || !feat || !y1) return fail(ECNF_E_INVALID, "NULL argument");
+  if (!h || !o) return fail(ECNF_E_INVALID, "NULL handle/options");
   if (batch < 0) return fail(ECNF_E_INVALID, "batch < 0");
+  if (batch > 0 && (!y0 || !feat || !y1)) return fail(ECNF_E_INVALID, "NULL argument");
   if (o->solver != ECNF_SOLVER_EULER && o->solver != ECNF_SOLVER_DOPRI5) return fail(ECNF_E_INVALID, "unknown solver");
   if (o->divergence < ECNF_DIV_NONE || o->divergence > ECNF_DIV_EXACT) return fail(ECNF_E_INVALID, "unknown divergence");
-  if (o->divergence == ECNF_DIV_HUTCHINSON && !eps) return fail(ECNF_E_INVALID, "Hutchinson divergence needs eps");
-  if (o->divergence != ECNF_DIV_NONE && !dlogp) return fail(ECNF_E_INVALID, "divergence requested but dlogp is NULL");
+  if (batch > 0 && o->divergence == ECNF_DIV_HUTCHINSON && !eps)
+    return fail(ECNF_E_INVALID, "Hutchinson divergence needs eps");
+  if (batch > 0 && o->divergence != ECNF_DIV_NONE && !dlogp)
+    return fail(ECNF_E_INVALID, "divergence requested but dlogp is NULL");
   if (o->t0 == o->t1) return fail(ECNF_E_INVALID, "t0 == t1");
   const bool adaptive = !(o->dt0 > 0.f);
   if (adaptive && o->solver == ECNF_SOLVER_EULER) return fail(ECNF_E_INVALID, "Euler has no error estimate: give dt0 > 0");
@@ -850,8 +859,9 @@ int ecnf_integrate(ecnf_handle* h, const ecnf_solve_opts* o, const float* y0, co
 }
 
 int ecnf_base_sample(ecnf_handle* h, const float* z, float* x0, int32_t batch, void* stream) {
-  if (!h || !z || !x0) return fail(ECNF_E_INVALID, "NULL argument");
+  if (!h) return fail(ECNF_E_INVALID, "NULL handle");
   if (batch <= 0) return batch == 0 ? ECNF_OK : fail(ECNF_E_INVALID, "batch < 0");
+  if (!z || !x0) return fail(ECNF_E_INVALID, "NULL argument");
   HIP_TRY(hipSetDevice(h->device));
   const int n = batch * h->cfg.dim;
   hipLaunchKernelGGL(base_sample_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, z, x0, batch,
@@ -861,8 +871,9 @@ int ecnf_base_sample(ecnf_handle* h, const float* z, float* x0, int32_t batch, v
 }
 
 int ecnf_base_log_prob(ecnf_handle* h, const float* y, float* log_p, int32_t batch, void* stream) {
-  if (!h || !y || !log_p) return fail(ECNF_E_INVALID, "NULL argument");
+  if (!h) return fail(ECNF_E_INVALID, "NULL handle");
   if (batch <= 0) return batch == 0 ? ECNF_OK : fail(ECNF_E_INVALID, "batch < 0");
+  if (!y || !log_p) return fail(ECNF_E_INVALID, "NULL argument");
   HIP_TRY(hipSetDevice(h->device));
   hipLaunchKernelGGL(base_log_prob_kernel, dim3((batch + 255) / 256), dim3(256), 0, (hipStream_t)stream, y, log_p,
                      batch, h->cfg.n_nodes, h->cfg.dim, h->cfg.base_scale);

@@ -100,7 +100,9 @@ class EcnfHandle:
         f = torch.as_tensor(feat, device=self.device)
         if f.dim() == 1:
             f = f.reshape(1, -1).expand(batch, -1)
-        f = f.reshape(batch, -1)
+        if f.numel() != batch * N:
+            raise ValueError(f"features must have {N} entries per molecule")
+        f = f.reshape(batch, N)
         if f.shape[1] != N:
             raise ValueError(f"features must have {N} entries per molecule, got {f.shape[1]}")
         if f.dtype.is_floating_point:

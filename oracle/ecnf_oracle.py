@@ -28,7 +28,8 @@ here and ``requirements.txt:1-16`` pins no versions):
 * diffrax (2023 API): ``Dopri5`` tableau with the Shampine embedded pair (b_error ends in -1/60), FSAL,
   ``ConstantStepSize`` (t_{n+1} = t_n + dt accumulated in fp32, clipped to t1 within 1e-6),
   ``PIDController`` defaults (I-controller, safety 0.9, factormin 0.2, factormax 10, error order 5,
-  rms norm over every leaf of the (x, logp) state, ``force_dtmin``) and Hairer's initial step
+  rms norm over every leaf of the state — (x, logp) for the joint solves, x alone for sample_cnf —
+  ``force_dtmin``) and Hairer's initial step
   selection; reversed time (t0 > t1) by reparametrisation tau = -t.
 * flax ``Dense``/``Embed`` (x @ kernel + bias, kernel [in, out]); e3nn-jax ``scatter_sum`` (segment sum);
   distrax ``ScalarAffine``/``Lambda``/``Transformed`` log-det conventions.
@@ -504,15 +505,17 @@ def odeint(field: _Field, x0, tau0: float, tau1: float, solver: str, dt0: Option
         kx0, kl0 = F(tau, x, idx_all)
         sx = f(atol) + np.abs(x) * f(rtol)
         sl = f(atol) + np.abs(lp) * f(rtol)
-        d0 = _rms([x / sx, (lp / sl)[:, None]])
-        d1 = _rms([kx0 / sx, (kl0 / sl)[:, None]])
+        # rms over the leaves of y: (x, logp) for the joint solves, x alone for sample_cnf (y0 = x0)
+        leaves = (lambda a, b: [a, b[:, None]]) if track_logp else (lambda a, b: [a])
+        d0 = _rms(leaves(x / sx, lp / sl))
+        d1 = _rms(leaves(kx0 / sx, kl0 / sl))
         cond = (d0 < 1e-5) | (d1 < 1e-5)
         d1s = np.where(cond, f(1), d1)
         h0 = np.where(cond, f(1e-6), f(0.01) * (d0 / d1s)).astype(dtype)
         x1 = x + h0[:, None] * kx0
         l1 = lp + h0 * kl0
         kx1, kl1 = F(tau + h0, x1, idx_all)
-        d2 = _rms([(kx1 - kx0) / sx, ((kl1 - kl0) / sl)[:, None]]) / h0
+        d2 = _rms(leaves((kx1 - kx0) / sx, (kl1 - kl0) / sl)) / h0
         maxd = np.maximum(d1, d2)
         h1 = np.where(maxd <= 1e-15, np.maximum(f(1e-6), h0 * f(1e-3)),
                       (f(0.01) / np.maximum(maxd, f(1e-30))) ** f(1 / 5)).astype(dtype)
@@ -559,7 +562,7 @@ def odeint(field: _Field, x0, tau0: float, tau1: float, solver: str, dt0: Option
         else:
             scx = f(atol) + np.maximum(np.abs(x0a), np.abs(x1)) * f(rtol)
             scl = f(atol) + np.maximum(np.abs(l0a), np.abs(l1)) * f(rtol)
-            err = _rms([ex / scx, (el / scl)[:, None]])
+            err = _rms([ex / scx, (el / scl)[:, None]] if track_logp else [ex / scx])
             keep = (err < 1) | at_dtmin[active]
             with np.errstate(divide="ignore"):
                 inv = f(1) / err
