@@ -167,7 +167,15 @@ __global__ __launch_bounds__(kThreads) void integrate_kernel(Net net, SolveP sp,
   int phase = sp.solver == ECNF_SOLVER_EULER ? kEuler : (sp.adaptive ? kInit0 : kFsal);
   int stage = 1;
 
+#ifdef ECNF_STAMPS
+  if (tid == 0) {
+    for (int i = 0; i < 32; ++i) s.stamps[i] = 0;
+    s.stamps[31] = __builtin_amdgcn_s_memtime();
+    s.stamps[30] = __builtin_amdgcn_s_memrealtime();
+  }
+#endif
   while (true) {
+    STAMP(s, kStSolver);
     // ------------------------------------------------ inputs of this evaluation
     float* kx_out;
     float* kl_out;
@@ -334,6 +342,15 @@ __global__ __launch_bounds__(kThreads) void integrate_kernel(Net net, SolveP sp,
     __syncthreads();
   }
   __syncthreads();
+#ifdef ECNF_STAMPS
+  if (tid == 0) {
+    STAMP(s, kStSolver);
+    s.stamps[29] = __builtin_amdgcn_s_memrealtime() - s.stamps[30];
+    for (int i = 0; i < kStCount; ++i) atomicAdd(&g_stamps[i], s.stamps[i]);
+    atomicAdd(&g_stamps[29], s.stamps[29]);
+    atomicAdd(&g_stamps[28], 1ull);
+  }
+#endif
   for (int i = tid; i < nmol * ND; i += kThreads) y1[(size_t)mol0 * ND + i] = st.y[i];
   if (tid < nmol) {
     if (dlogp) dlogp[mol0 + tid] = st.lp[tid];
@@ -623,6 +640,19 @@ hipError_t dispatch_vf(const ecnf_handle* h, int NT, const float* x, const float
 extern "C" {
 
 int ecnf_abi_version(void) { return ECNF_ABI_VERSION; }
+
+#ifdef ECNF_STAMPS
+// diagnostic build only: copy (and optionally reset) the accumulated phase cycles
+int ecnf_debug_stamps(unsigned long long* out, int n, int reset) {
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * std::min(n, 32)));
+  if (reset) {
+    unsigned long long z[32] = {0};
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof(z)));
+  }
+  return ECNF_OK;
+}
+#endif
 
 const char* ecnf_last_error(void) { return g_err.c_str(); }
 

@@ -18,9 +18,9 @@
 //     pre-packed on the host into lane order (one dwordx4 per lane = 4 A fragments).
 //   * phi_e layer 1 is factorised: [h_s | h_r | d^2] W = (h W_s)[s] + (h W_r + b)[r] + d^2 w_d; the per-node
 //     halves are one node GEMM into LDS and are gathered per edge.
-//   * segment sums (e3nn.scatter_sum over the contiguous receiver runs) are segmented suffix scans with
-//     __shfl_down inside each 32-edge tile followed by one LDS add per (segment, tile); a node's N-1 <= 32 edges
-//     touch at most two tiles and 0 + a + b == 0 + b + a, so the result is run-to-run deterministic.
+//   * segment sums (e3nn.scatter_sum over the contiguous receiver runs) are segmented prefix scans in DPP
+//     (row_shr / row_bcast:15) inside each 32-edge tile followed by one LDS add per (segment, tile); a node's
+//     N-1 <= 32 edges touch at most two tiles and 0 + a + b == 0 + b + a, so the result is run-to-run deterministic.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -35,6 +35,14 @@ constexpr int kMaxHalfT = 8;    // T <= 16
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// global (address space 1) views of the weight buffers: global_load_* with counted vmcnt waits instead of flat
+// loads, which hipcc must fence with vmcnt(0) lgkmcnt(0)
+#define ECNF_GLOBAL __attribute__((address_space(1)))
+typedef const ECNF_GLOBAL float* gfloat_p;
+typedef const ECNF_GLOBAL f32x4* gf32x4_p;
+__device__ __forceinline__ gfloat_p gptr(const float* p) { return (gfloat_p)(p); }
+__device__ __forceinline__ gf32x4_p gptr4(const float* p) { return (gf32x4_p)(p); }
 
 struct BlockW {
   const float* Wn;  const float* bn;    // node Dense [(H+T)][H], [H]           (egnn.py:166-167)
@@ -63,6 +71,40 @@ struct Net {
 };
 
 // ---------------------------------------------------------------------------------------------------
+// diagnostic phase stamps (separate build, -DECNF_STAMPS): thread 0 of every workgroup adds the shader-clock
+// cycles of each barrier-delimited phase into LDS slots; the kernel flushes them to g_stamps at exit.
+// Never compiled into the product library.
+// ---------------------------------------------------------------------------------------------------
+enum StampSlot {
+  kStPrologue = 0, kStNodeDense, kStPGemm, kStEdge, kStNodeUpd, kStPhiH, kStEpilogue, kStSolver,
+  kStEdgeChainE, kStEdgeTail, kStEdgeLayer1, kStCount
+};
+#ifdef ECNF_STAMPS
+__device__ unsigned long long g_stamps[32];
+#define ECNF_STAMP_DECL unsigned long long* stamps;
+#define STAMP(s, slot)                                                    \
+  do {                                                                    \
+    if (threadIdx.x == 0) {                                               \
+      unsigned long long t_ = __builtin_amdgcn_s_memtime();               \
+      (s).stamps[slot] += t_ - (s).stamps[31];                            \
+      (s).stamps[31] = t_;                                                \
+    }                                                                     \
+  } while (0)
+#define STAMP_LANE0(s, slot, t0)                                          \
+  do {                                                                    \
+    if (threadIdx.x == 0) {                                               \
+      unsigned long long t_ = __builtin_amdgcn_s_memtime();               \
+      (s).stamps[slot] += t_ - (t0);                                      \
+      (t0) = t_;                                                          \
+    }                                                                     \
+  } while (0)
+#else
+#define ECNF_STAMP_DECL
+#define STAMP(s, slot) do {} while (0)
+#define STAMP_LANE0(s, slot, t0) do {} while (0)
+#endif
+
+// ---------------------------------------------------------------------------------------------------
 // LDS carve-up
 // ---------------------------------------------------------------------------------------------------
 struct Lds {
@@ -77,6 +119,7 @@ struct Lds {
   float* temb;               // [MPW][T]
   int*   feat;               // [MPW][N]
   float* tail;               // first free float (solver state follows)
+  ECNF_STAMP_DECL
 };
 
 __host__ __device__ inline int align4(int n) { return (n + 3) & ~3; }
@@ -93,6 +136,9 @@ __host__ __device__ inline int lds_eval_floats(int N, int D, int H, int T, int M
   n += align4(2 * MPW * D);
   n += align4(MPW * T);
   n += align4(MPW * N);
+#ifdef ECNF_STAMPS
+  n += 64;   // 32 x u64 stamp slots
+#endif
   return n;
 }
 
@@ -111,6 +157,9 @@ __device__ inline Lds carve_lds(const Net& net, float* base) {
   s.mean = p;  p += align4(2 * net.MPW * net.D);
   s.temb = p;  p += align4(net.MPW * net.T);
   s.feat = reinterpret_cast<int*>(p); p += align4(net.MPW * net.N);
+#ifdef ECNF_STAMPS
+  s.stamps = reinterpret_cast<unsigned long long*>(p); p += 64;
+#endif
   s.tail = p;
   return s;
 }
@@ -140,6 +189,8 @@ __device__ __forceinline__ const float* launder_uniform(const float* p) {
   return reinterpret_cast<const float*>(((uint64_t)hi << 32) | lo);
 }
 
+__device__ __forceinline__ f32x4 ldg4(const float* p, int idx4) { return gptr4(p)[idx4]; }
+
 __device__ __forceinline__ f32x16 mfma32(float a, float b, const f32x16& c) {
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
@@ -150,11 +201,61 @@ __device__ __forceinline__ int acc_row(int r, int kk) { return (r & 3) + 8 * (r 
 __device__ __forceinline__ void init_bias(f32x16& acc, const float* __restrict__ bias, int jb, int kk) {
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    f32x4 b = bias ? *reinterpret_cast<const f32x4*>(bias + jb * 32 + 8 * q + 4 * kk) : f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 b = bias ? gptr4(bias + jb * 32 + 8 * q + 4 * kk)[0] : f32x4{0.f, 0.f, 0.f, 0.f};
     acc[4 * q + 0] = b[0];
     acc[4 * q + 1] = b[1];
     acc[4 * q + 2] = b[2];
     acc[4 * q + 3] = b[3];
+  }
+}
+
+// ---------------------------------------------------------------------------------------------------
+// node GEMM k-loop over one source: acc += sum_k W[k][jb*32+i] X[n][k] for k in [0, K).  A (global) and B (LDS)
+// fragments are software-pipelined one chunk of CH k-steps ahead, so neither the L2 nor the LDS latency sits
+// between dependent MFMAs.
+// ---------------------------------------------------------------------------------------------------
+template <int NT>
+__device__ __forceinline__ void node_kloop(f32x16& acc, f32x16& accT, gfloat_p wcol, int ldw, const float* xr,
+                                           const float* xrT, int K) {
+  constexpr int CH = 8;
+  const int nks = K >> 1;              // k-steps of 2
+  const int nch = nks / CH;
+  float an[CH], bn[CH], btn[CH];
+  if (nch > 0) {
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+      an[j] = wcol[(2 * j) * ldw];
+      bn[j] = xr[2 * j];
+      if constexpr (NT) btn[j] = xrT[2 * j];
+    }
+  }
+  for (int c = 0; c < nch; ++c) {
+    float ac[CH], bc[CH], btc[CH];
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+      ac[j] = an[j];
+      bc[j] = bn[j];
+      if constexpr (NT) btc[j] = btn[j];
+    }
+    if (c + 1 < nch) {
+      const int k0 = 2 * CH * (c + 1);
+#pragma unroll
+      for (int j = 0; j < CH; ++j) {
+        an[j] = wcol[(k0 + 2 * j) * ldw];
+        bn[j] = xr[k0 + 2 * j];
+        if constexpr (NT) btn[j] = xrT[k0 + 2 * j];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+      acc = mfma32(ac[j], bc[j], acc);
+      if constexpr (NT) accT = mfma32(ac[j], btc[j], accT);
+    }
+  }
+  for (int k = 2 * CH * nch; k < K; k += 2) {
+    const float a = wcol[k * ldw];
+    acc = mfma32(a, xr[k], acc);
+    if constexpr (NT) accT = mfma32(a, xrT[k], accT);
   }
 }
 
@@ -174,32 +275,11 @@ __device__ __forceinline__ void node_gemm(const float* X1, int ldx1, int K1, con
     const int n = ct * 32 + li;
     f32x16 acc, accT;
     init_bias(acc, bias, jb, kk);
-    if constexpr (NT) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) accT[r] = 0.f;
-    }
-    const float* wcol = W + kk * ldw + jb * 32 + li;
-    {
-      const float* xr = X1 + n * ldx1 + kk;
-      const float* xrT = X1 + (RP + n) * ldx1 + kk;
-#pragma unroll 4
-      for (int k = 0; k < K1; k += 2) {
-        const float a = wcol[k * ldw];
-        acc = mfma32(a, xr[k], acc);
-        if constexpr (NT) accT = mfma32(a, xrT[k], accT);
-      }
-    }
-    if (K2 > 0) {
-      const float* w2 = wcol + K1 * ldw;
-      const float* xr = X2 + n * ldx2 + kk;
-      const float* xrT = X2 + (RP + n) * ldx2 + kk;
-#pragma unroll 4
-      for (int k = 0; k < K2; k += 2) {
-        const float a = w2[k * ldw];
-        acc = mfma32(a, xr[k], acc);
-        if constexpr (NT) accT = mfma32(a, xrT[k], accT);
-      }
-    }
+    for (int r = 0; r < 16; ++r) accT[r] = 0.f;
+    const gfloat_p wcol = gptr(W) + kk * ldw + jb * 32 + li;
+    node_kloop<NT>(acc, accT, wcol, ldw, X1 + n * ldx1 + kk, X1 + (RP + n) * ldx1 + kk, K1);
+    if (K2 > 0) node_kloop<NT>(acc, accT, wcol + K1 * ldw, ldw, X2 + n * ldx2 + kk, X2 + (RP + n) * ldx2 + kk, K2);
     if (n < nvalid) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
@@ -222,40 +302,55 @@ __device__ __forceinline__ void node_gemm(const float* X1, int ldx1, int K1, con
 }
 
 // ---------------------------------------------------------------------------------------------------
-// edge-MLP chain layer: b = silu(a W + bias), all in registers (a, b: NF blocks of 32 rows x 32 edges)
+// edge-MLP chain layer: b = silu(a W + bias), all in registers (a, b: NF blocks of 32 rows x 32 edges).
+// The A fragments of one (output block jb, input block fb) group are 4 dwordx4 per lane (16 MFMAs); groups are
+// software-pipelined PF groups ahead so the L2 latency hides behind MFMAs (counted vmcnt, no vmcnt(0) stalls).
 // ---------------------------------------------------------------------------------------------------
 template <int NF, int NT>
 __device__ __forceinline__ void chain_layer(const f32x16 (&a)[NF], const f32x16 (&aT)[NF], f32x16 (&b)[NF],
                                             f32x16 (&bT)[NF], const float* __restrict__ Wpk,
                                             const float* __restrict__ bias, int lane) {
+  constexpr int NG = NF * NF;           // weight groups per layer
+  constexpr int PF = NT ? 1 : 2;        // groups in flight ahead of the MFMAs
   const int kk = lane >> 5;
+  const gf32x4_p wp = gptr4(Wpk) + lane;
+  f32x4 wbuf[PF + 1][4];
 #pragma unroll
-  for (int jb = 0; jb < NF; ++jb) {
-    f32x16 acc, accT;
-    init_bias(acc, bias, jb, kk);
-    if constexpr (NT) {
+  for (int g = 0; g < PF && g < NG; ++g)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) accT[r] = 0.f;
+    for (int q = 0; q < 4; ++q) wbuf[g][q] = wp[(g * 4 + q) * 64];
+  f32x16 acc, accT;
+#pragma unroll
+  for (int g = 0; g < NG; ++g) {
+    const int jb = g / NF, fb = g % NF;
+    if (g + PF < NG) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) wbuf[(g + PF) % (PF + 1)][q] = wp[((g + PF) * 4 + q) * 64];
     }
-    const f32x4* wp = reinterpret_cast<const f32x4*>(Wpk) + (jb * NF * 4) * 64 + lane;
+    if (fb == 0) {
+      init_bias(acc, bias, jb, kk);
+      if constexpr (NT) {
 #pragma unroll
-    for (int fb = 0; fb < NF; ++fb) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const f32x4 w = wp[(fb * 4 + q) * 64];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          acc = mfma32(w[e], a[fb][4 * q + e], acc);
-          if constexpr (NT) accT = mfma32(w[e], aT[fb][4 * q + e], accT);
-        }
+        for (int r = 0; r < 16; ++r) accT[r] = 0.f;
       }
     }
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      float y, yT = 0.f;
-      silu_dual<NT>(acc[r], NT ? accT[r] : 0.f, y, yT);
-      b[jb][r] = y;
-      if constexpr (NT) bT[jb][r] = yT;
+    for (int q = 0; q < 4; ++q) {
+      const f32x4 w = wbuf[g % (PF + 1)][q];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        acc = mfma32(w[e], a[fb][4 * q + e], acc);
+        if constexpr (NT) accT = mfma32(w[e], aT[fb][4 * q + e], accT);
+      }
+    }
+    if (fb == NF - 1) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float y, yT = 0.f;
+        silu_dual<NT>(acc[r], NT ? accT[r] : 0.f, y, yT);
+        b[jb][r] = y;
+        if constexpr (NT) bT[jb][r] = yT;
+      }
     }
   }
 }
@@ -275,27 +370,47 @@ struct Chain<NF, NT, 0> {
                                              const float*, const float*, int) {}
 };
 
-// segmented (by receiver row) suffix sum over the 32 edge lanes of a half-wave
+// Segmented (by receiver row) inclusive PREFIX sum over the 32 edge lanes of each half-wave, in DPP:
+// row_shr:1,2,4,8 inside each 16-lane row, then row_bcast:15 carries lane 15's running sum into lanes 16..31
+// (rows 1 and 3 only, so the two half-waves — same edges, different feature rows — never mix).  Each step is
+// v += ok_step * dpp(v): a mov_dpp and an fma per value, no LDS traffic and no waits.  Segments are contiguous
+// lane runs, so "same segment as the source lane" is the Hillis-Steele condition; the tail lane of a segment
+// ends holding the segment's sum inside this tile.
 struct SegScan {
-  bool ok[5];
-  bool head;
-  __device__ __forceinline__ void init(int seg, int li) {
-#pragma unroll
-    for (int o = 0; o < 5; ++o) {
-      const int off = 1 << o;
-      const int other = __shfl_down(seg, off, 32);
-      ok[o] = (li + off < 32) && (other == seg);
-    }
-    const int prev = __shfl_up(seg, 1, 32);
-    head = (li == 0) || (prev != seg);
+  float okf[5];
+  bool tail;
+  template <int CTRL, int ROWMASK>
+  __device__ __forceinline__ static int dpp_i(int v) {
+    return __builtin_amdgcn_update_dpp(0, v, CTRL, ROWMASK, 0xF, true);
   }
-  __device__ __forceinline__ float sum(float v) const {
+  template <int CTRL, int ROWMASK>
+  __device__ __forceinline__ static float dpp_f(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, ROWMASK, 0xF,
+                                                                  true));
+  }
+  __device__ __forceinline__ void init(int seg, int li) {
+    const int sp = seg + 1;   // 0 marks "no source lane" (bound_ctrl / masked rows read 0)
+    int src;
+    src = dpp_i<0x111, 0xF>(sp); okf[0] = (sp != 0 && src == sp) ? 1.f : 0.f;   // row_shr:1
+    src = dpp_i<0x112, 0xF>(sp); okf[1] = (sp != 0 && src == sp) ? 1.f : 0.f;   // row_shr:2
+    src = dpp_i<0x114, 0xF>(sp); okf[2] = (sp != 0 && src == sp) ? 1.f : 0.f;   // row_shr:4
+    src = dpp_i<0x118, 0xF>(sp); okf[3] = (sp != 0 && src == sp) ? 1.f : 0.f;   // row_shr:8
+    src = dpp_i<0x142, 0xA>(sp); okf[4] = (sp != 0 && src == sp) ? 1.f : 0.f;   // row_bcast:15 -> rows 1, 3
+    const int nxt = __shfl_down(seg, 1, 32);
+    tail = (li == 31) || (nxt != seg);
+  }
+  template <int NV>
+  __device__ __forceinline__ void sum_many(float (&v)[NV]) const {
 #pragma unroll
-    for (int o = 0; o < 5; ++o) {
-      const float w = __shfl_down(v, 1 << o, 32);
-      v = ok[o] ? v + w : v;
-    }
-    return v;
+    for (int i = 0; i < NV; ++i) v[i] = fmaf(okf[0], dpp_f<0x111, 0xF>(v[i]), v[i]);
+#pragma unroll
+    for (int i = 0; i < NV; ++i) v[i] = fmaf(okf[1], dpp_f<0x112, 0xF>(v[i]), v[i]);
+#pragma unroll
+    for (int i = 0; i < NV; ++i) v[i] = fmaf(okf[2], dpp_f<0x114, 0xF>(v[i]), v[i]);
+#pragma unroll
+    for (int i = 0; i < NV; ++i) v[i] = fmaf(okf[3], dpp_f<0x118, 0xF>(v[i]), v[i]);
+#pragma unroll
+    for (int i = 0; i < NV; ++i) v[i] = fmaf(okf[4], dpp_f<0x142, 0xA>(v[i]), v[i]);
   }
 };
 
@@ -316,7 +431,7 @@ __device__ __forceinline__ void edge_shift(const Net& net, const BlockW& bw, con
   for (int fb = 0; fb < NF; ++fb)
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const f32x4 w = *reinterpret_cast<const f32x4*>(bw.wx + fb * 32 + 8 * q + 4 * kk);
+      const f32x4 w = gptr4(bw.wx + fb * 32 + 8 * q + 4 * kk)[0];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         phx += w[e] * px[fb][4 * q + e];
@@ -328,13 +443,18 @@ __device__ __forceinline__ void edge_shift(const Net& net, const BlockW& bw, con
   phx += bw.bx;
   const float den = net.C + length;
   const int RP = net.RP;
+  float sh[2 * D];
 #pragma unroll
   for (int d = 0; d < D; ++d) {
-    const float sh = sc.sum((phx * r[d]) / den);
-    if (writer && kk == 0) lds_add(&s.dxacc[rr * D + d], sh);
-    if constexpr (NT) {
-      const float shT = sc.sum((phxT * r[d] + phx * dr[d]) / den - (phx * r[d]) * dlength / (den * den));
-      if (writer && kk == 0) lds_add(&s.dxacc[(RP + rr) * D + d], shT);
+    sh[d] = (phx * r[d]) / den;
+    sh[D + d] = NT ? (phxT * r[d] + phx * dr[d]) / den - (phx * r[d]) * dlength / (den * den) : 0.f;
+  }
+  sc.sum_many<2 * D>(sh);
+  if (writer && kk == 0) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      lds_add(&s.dxacc[rr * D + d], sh[d]);
+      if constexpr (NT) lds_add(&s.dxacc[(RP + rr) * D + d], sh[D + d]);
     }
   }
 }
@@ -352,7 +472,7 @@ __device__ __forceinline__ void edge_tail(const Net& net, const BlockW& bw, cons
   for (int fb = 0; fb < NF; ++fb)
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const f32x4 w = *reinterpret_cast<const f32x4*>(bw.wg + fb * 32 + 8 * q + 4 * kk);
+      const f32x4 w = gptr4(bw.wg + fb * 32 + 8 * q + 4 * kk)[0];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         part += w[e] * m[fb][4 * q + e];
@@ -367,20 +487,29 @@ __device__ __forceinline__ void edge_tail(const Net& net, const BlockW& bw, cons
   // m_i = scatter_sum(m_ij * e_ij) (the / sqrt(N-1) happens in the node update)   (egnn.py:102-104)
   SegScan sc;
   sc.init(valid ? rr : -1, li);
-  const bool writer = valid && sc.head;
+  const bool writer = valid && sc.tail;
   const int RP = net.RP;
 #pragma unroll
-  for (int fb = 0; fb < NF; ++fb)
+  for (int fb = 0; fb < NF; ++fb) {
+    float v[16];
 #pragma unroll
-    for (int r16 = 0; r16 < 16; ++r16) {
-      const int row = fb * 32 + acc_row(r16, kk);
-      const float v = sc.sum(m[fb][r16] * g);
-      if (writer) lds_add(&s.macc[rr * s.ld_m + row], v);
-      if constexpr (NT) {
-        const float vT = sc.sum(gT * m[fb][r16] + g * mT[fb][r16]);
-        if (writer) lds_add(&s.macc[(RP + rr) * s.ld_m + row], vT);
+    for (int r16 = 0; r16 < 16; ++r16) v[r16] = m[fb][r16] * g;
+    sc.sum_many<16>(v);
+    if (writer) {
+#pragma unroll
+      for (int r16 = 0; r16 < 16; ++r16) lds_add(&s.macc[rr * s.ld_m + fb * 32 + acc_row(r16, kk)], v[r16]);
+    }
+    if constexpr (NT) {
+#pragma unroll
+      for (int r16 = 0; r16 < 16; ++r16) v[r16] = gT * m[fb][r16] + g * mT[fb][r16];
+      sc.sum_many<16>(v);
+      if (writer) {
+#pragma unroll
+        for (int r16 = 0; r16 < 16; ++r16)
+          lds_add(&s.macc[(RP + rr) * s.ld_m + fb * 32 + acc_row(r16, kk)], v[r16]);
       }
     }
+  }
 
   // phi_x torso (egnn.py:82) then its Dense(1) and the shifts
   const float* We = bw.We + (L - 1) * NF * NF * 1024;
@@ -410,6 +539,9 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
   int sd = i + 1 + jj;
   if (sd >= N) sd -= N;
   const int rr = mol * N + i, rs = mol * N + sd;   // receiver / sender rows (graph.py:10-13)
+#ifdef ECNF_STAMPS
+  unsigned long long t_sub = __builtin_amdgcn_s_memtime();
+#endif
 
   // r_ij = x_i - x_j, lengths = safe_norm (egnn.py:73-74, numerical.py:7-10)
   float r[D], dr[D];
@@ -447,7 +579,7 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
   for (int fb = 0; fb < NF; ++fb)
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const f32x4 w = *reinterpret_cast<const f32x4*>(bw.wd + fb * 32 + 8 * q + 4 * kk);
+      const f32x4 w = gptr4(bw.wd + fb * 32 + 8 * q + 4 * kk)[0];
 #pragma unroll
       for (int e4 = 0; e4 < 4; ++e4) {
         const int row = fb * 32 + 8 * q + 4 * kk + e4;
@@ -463,15 +595,18 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
         X0[fb][4 * q + e4] = y;
       }
     }
+  STAMP_LANE0(s, kStEdgeLayer1, t_sub);
   // phi_e layers 2..L.  The weight pointer is laundered through an empty asm so the (tile-invariant) weight
   // loads are not hoisted out of the tile loop into thousands of live registers.
   const float* We = launder_uniform(bw.We);
   Chain<NF, NT, L - 1>::run(X0, T0, X1, T1, We, bw.be, lane);
+  STAMP_LANE0(s, kStEdgeChainE, t_sub);
   if constexpr ((L - 1) % 2 == 0) {
     edge_tail<NF, NT, L, D>(net, bw, s, X0, T0, X1, T1, valid, rr, r, dr, length, dlength, lane);
   } else {
     edge_tail<NF, NT, L, D>(net, bw, s, X1, T1, X0, T0, valid, rr, r, dr, length, dlength, lane);
   }
+  STAMP_LANE0(s, kStEdgeTail, t_sub);
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -515,11 +650,12 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
     float v = 0.f;
     if (row < nvalid) {
       const int m = row / N;
-      v = c < H ? net.emb[s.feat[row] * H + c] : s.temb[m * T + (c - H)];
+      v = c < H ? gptr(net.emb)[s.feat[row] * H + c] : s.temb[m * T + (c - H)];
     }
     s.hin[row * s.ld_hin + c] = v;
   }
   __syncthreads();
+  STAMP(s, kStPrologue);
 
   const int ntiles = (MPW * net.EP) >> 5;
   for (int k = 0; k < net.K; ++k) {
@@ -528,13 +664,16 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
     node_gemm<NT>(s.hin, s.ld_hin, H + T, nullptr, 0, 0, bw.Wn, H, bw.bn, H, false, nullptr, 0, s.hb, s.ld_hb, RP,
                   nvalid, wave, lane);
     __syncthreads();
+    STAMP(s, kStNodeDense);
     // per-node halves of phi_e layer 1
     node_gemm<NT>(s.hb, s.ld_hb, H, nullptr, 0, 0, bw.Wp, 2 * M, bw.bp, 2 * M, false, nullptr, 0, s.P, s.ld_P, RP,
                   nvalid, wave, lane);
     __syncthreads();
+    STAMP(s, kStPGemm);
     // edges
     for (int tile = wave; tile < ntiles; tile += kWaves) edge_tile<NF, NT, L, D>(net, bw, s, tile, lane);
     __syncthreads();
+    STAMP(s, kStEdge);
     // node update: x += shift_i / (N-1) (egnn.py:95,113); m_i /= sqrt(N-1) (egnn.py:104)
     for (int idx = tid; idx < R * D; idx += kThreads) {
       s.xc[idx] += s.dxacc[idx] / net.nn1;
@@ -545,6 +684,7 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
       s.macc[row * s.ld_m + c] /= net.sqrt_nn1;
     }
     __syncthreads();
+    STAMP(s, kStNodeUpd);
     // phi_h = MLP((M,)*L + (H,)) on [m_i | h], residual (egnn.py:105-111)
     float* Q0 = s.P;
     float* Q1 = s.P + (M + 1);
@@ -564,6 +704,7 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
     node_gemm<NT>(Q0, s.ld_P, M, nullptr, 0, 0, bw.Wh[L], H, bw.bh[L], H, false, s.hb, s.ld_hb, s.hin, s.ld_hin, RP,
                   nvalid, wave, lane);
     __syncthreads();
+    STAMP(s, kStPhiH);
   }
 
   // ---- epilogue: v = ((x_K - x_c0) - mean(x_in)) * final_scaling  (egnn.py:183-188) ----
@@ -576,6 +717,7 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
     dst[m * ND + (n - m * N) * D + d] = v;
   }
   __syncthreads();
+  STAMP(s, kStEpilogue);
 }
 
 }  // namespace ecnf

@@ -4,7 +4,7 @@ Tolerances (fp32 kernel vs fp64 oracle; stated per test):
   * one vector-field evaluation / JVP: max |err| <= 2e-5 * max(1, max |ref|)
   * fixed-step trajectories (100 Euler steps, 20 Dopri5 steps): max |err| <= 1e-4
   * adaptive Dopri5: step sequences fork in fp32, so the kernel must be within 2x the oracle's own distance to an
-    accurate fp64 fixed-step solution, NFE within 35 % of the oracle's
+    accurate fp64 fixed-step solution, batch-mean NFE within 30 % of the oracle's
   * log-densities: |err| <= 2e-3 absolute (values are O(10-100))
 """
 import numpy as np
@@ -175,7 +175,7 @@ def test_dopri5_adaptive_sample(name):
     """PIDController(rtol=atol=1e-5) solves fork in their accept/reject sequences under fp32 rounding, so the
     kernel is held to the accuracy of the oracle's own adaptive solve: both are compared to an accurate
     fixed-step fp64 solution (Dopri5, dt = 0.005) and the kernel may be at most 2x (+2e-4) further from it;
-    NFE must lie within 35 % of the oracle's."""
+    the batch-mean NFE must lie within 30 % of the oracle's."""
     cfg = CONFIGS[name]
     oc, params, h, z, x0, feat = setup(cfg, B=5)
     y1, _, nfe, _ = h.integrate(g(x0), g(feat, torch.int32), 0.0, 1.0, SolveOptions("dopri5", None))
@@ -184,8 +184,10 @@ def test_dopri5_adaptive_sample(name):
     err_k = np.abs(y1.cpu().numpy() - fine).max()
     err_o = np.abs(ref - fine).max()
     assert err_k <= 2 * err_o + 2e-4, (err_k, err_o)
+    # per-molecule step counts are chaotic under 1e-7 input perturbations (the oracle's own NFE for one ALDP
+    # molecule spans 147-309), so the NFE check is on the batch mean
     nfe = nfe.cpu().numpy()
-    assert np.all(np.abs(nfe - nfe_ref) <= 0.35 * nfe_ref), (nfe, nfe_ref)
+    assert abs(nfe.mean() - nfe_ref.mean()) <= 0.3 * nfe_ref.mean(), (nfe, nfe_ref)
 
 
 def test_log_prob_exact_fixed():

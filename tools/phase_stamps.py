@@ -1,0 +1,44 @@
+"""Diagnostic: per-phase shader-cycle shares of integrate_kernel (LJ13 B=1024 Euler NFE=100) from the
+-DECNF_STAMPS build (tools/build_stamps.sh).  Shares are read from workgroup thread 0 at barrier boundaries."""
+import ctypes
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "ecnf-baseline-neurips-2023_amd"))
+os.environ["ECNF_LIB"] = os.path.join(ROOT, "tools", "libecnf_hip_stamps.so")
+
+import torch  # noqa: E402
+from ecnf_amd import CONFIGS, init_params, _lib  # noqa: E402
+from ecnf_amd.engine import EcnfHandle, SolveOptions  # noqa: E402
+
+NAMES = ["prologue", "node_dense", "p_gemm", "edge", "node_update", "phi_h", "epilogue", "solver",
+         "edge_chain_e(w0)", "edge_tail(w0)", "edge_layer1(w0)"]
+name = sys.argv[1] if len(sys.argv) > 1 else "lj13"
+B = int(sys.argv[2]) if len(sys.argv) > 2 else 1024
+cfg = CONFIGS[name]
+h = EcnfHandle(cfg, init_params(cfg, 0), 0)
+lib = h.lib
+lib.ecnf_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+z = torch.randn((B, cfg.event_dim), device="cuda")
+x0 = h.base_sample(z)
+feat = torch.zeros((B, cfg.n_nodes), device="cuda", dtype=torch.int32)
+h.integrate(x0, feat, 0.0, 1.0, SolveOptions("euler", 0.01))
+buf = (ctypes.c_ulonglong * 32)()
+lib.ecnf_debug_stamps(buf, 32, 1)
+ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+ev0.record()
+h.integrate(x0, feat, 0.0, 1.0, SolveOptions("euler", 0.01))
+ev1.record()
+torch.cuda.synchronize()
+lib.ecnf_debug_stamps(buf, 32, 1)
+nwg = buf[28]
+cyc = [buf[i] / nwg for i in range(len(NAMES))]
+tot = sum(cyc[:8])
+real_us = buf[29] / nwg / 100.0   # s_memrealtime is 100 MHz
+out = {"config": name, "batch": B, "workgroups": nwg, "kernel_ms": ev0.elapsed_time(ev1),
+       "cycles_per_wg": tot, "wg_wall_us": real_us, "clock_GHz": tot / (real_us * 1e3),
+       "shares": {n: cyc[i] / tot for i, n in enumerate(NAMES[:8])},
+       "edge_wave0_shares_of_edge": {n: cyc[i] / max(cyc[3], 1) for i, n in list(enumerate(NAMES))[8:]}}
+print(json.dumps(out, indent=1))
