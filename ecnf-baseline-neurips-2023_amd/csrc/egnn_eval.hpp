@@ -117,6 +117,7 @@ struct Lds {
   float* dxacc;              // [R][D]    shift aggregate
   float* mean;               // [2][MPW][D] input mean (primal, tangent)
   float* temb;               // [MPW][T]
+  float* vecs;               // [(2L-1) + 3][M] this block's chain biases, w_d, w_g, w_x (staged once per block)
   int*   feat;               // [MPW][N]
   float* tail;               // first free float (solver state follows)
   ECNF_STAMP_DECL
@@ -135,6 +136,7 @@ __host__ __device__ inline int lds_eval_floats(int N, int D, int H, int T, int M
   n += 3 * align4(R * D);
   n += align4(2 * MPW * D);
   n += align4(MPW * T);
+  n += align4((2 * 4 + 2) * M);   // vecs, sized for L <= 4
   n += align4(MPW * N);
 #ifdef ECNF_STAMPS
   n += 64;   // 32 x u64 stamp slots
@@ -156,6 +158,7 @@ __device__ inline Lds carve_lds(const Net& net, float* base) {
   s.dxacc = p; p += align4(R * net.D);
   s.mean = p;  p += align4(2 * net.MPW * net.D);
   s.temb = p;  p += align4(net.MPW * net.T);
+  s.vecs = p;  p += align4((2 * 4 + 2) * net.M);
   s.feat = reinterpret_cast<int*>(p); p += align4(net.MPW * net.N);
 #ifdef ECNF_STAMPS
   s.stamps = reinterpret_cast<unsigned long long*>(p); p += 64;
@@ -210,30 +213,32 @@ __device__ __forceinline__ void init_bias(f32x16& acc, const float* __restrict__
 }
 
 // ---------------------------------------------------------------------------------------------------
-// node GEMM k-loop over one source: acc += sum_k W[k][jb*32+i] X[n][k] for k in [0, K).  A (global) and B (LDS)
-// fragments are software-pipelined one chunk of CH k-steps ahead, so neither the L2 nor the LDS latency sits
-// between dependent MFMAs.
+// node GEMM k-loop over one source: acc[a] += sum_k W[k][(jb + a)*32 + i] X[n][k] for k in [0, K), NA output
+// blocks sharing every B fragment.  A (global) and B (LDS) fragments are software-pipelined one chunk of CH
+// k-steps ahead, so neither the L2 nor the LDS latency sits between dependent MFMAs.
 // ---------------------------------------------------------------------------------------------------
-template <int NT>
-__device__ __forceinline__ void node_kloop(f32x16& acc, f32x16& accT, gfloat_p wcol, int ldw, const float* xr,
-                                           const float* xrT, int K) {
+template <int NT, int NA>
+__device__ __forceinline__ void node_kloop(f32x16 (&acc)[NA], f32x16 (&accT)[NA], gfloat_p wcol, int ldw,
+                                           const float* xr, const float* xrT, int K) {
   constexpr int CH = 8;
   const int nks = K >> 1;              // k-steps of 2
   const int nch = nks / CH;
-  float an[CH], bn[CH], btn[CH];
+  float an[NA][CH], bn[CH], btn[CH];
   if (nch > 0) {
 #pragma unroll
     for (int j = 0; j < CH; ++j) {
-      an[j] = wcol[(2 * j) * ldw];
+#pragma unroll
+      for (int a = 0; a < NA; ++a) an[a][j] = wcol[(2 * j) * ldw + 32 * a];
       bn[j] = xr[2 * j];
       if constexpr (NT) btn[j] = xrT[2 * j];
     }
   }
   for (int c = 0; c < nch; ++c) {
-    float ac[CH], bc[CH], btc[CH];
+    float ac[NA][CH], bc[CH], btc[CH];
 #pragma unroll
     for (int j = 0; j < CH; ++j) {
-      ac[j] = an[j];
+#pragma unroll
+      for (int a = 0; a < NA; ++a) ac[a][j] = an[a][j];
       bc[j] = bn[j];
       if constexpr (NT) btc[j] = btn[j];
     }
@@ -241,54 +246,62 @@ __device__ __forceinline__ void node_kloop(f32x16& acc, f32x16& accT, gfloat_p w
       const int k0 = 2 * CH * (c + 1);
 #pragma unroll
       for (int j = 0; j < CH; ++j) {
-        an[j] = wcol[(k0 + 2 * j) * ldw];
+#pragma unroll
+        for (int a = 0; a < NA; ++a) an[a][j] = wcol[(k0 + 2 * j) * ldw + 32 * a];
         bn[j] = xr[k0 + 2 * j];
         if constexpr (NT) btn[j] = xrT[k0 + 2 * j];
       }
     }
 #pragma unroll
     for (int j = 0; j < CH; ++j) {
-      acc = mfma32(ac[j], bc[j], acc);
-      if constexpr (NT) accT = mfma32(ac[j], btc[j], accT);
+#pragma unroll
+      for (int a = 0; a < NA; ++a) {
+        acc[a] = mfma32(ac[a][j], bc[j], acc[a]);
+        if constexpr (NT) accT[a] = mfma32(ac[a][j], btc[j], accT[a]);
+      }
     }
   }
   for (int k = 2 * CH * nch; k < K; k += 2) {
-    const float a = wcol[k * ldw];
-    acc = mfma32(a, xr[k], acc);
-    if constexpr (NT) accT = mfma32(a, xrT[k], accT);
+    const float b = xr[k];
+    const float bt = NT ? xrT[k] : 0.f;
+#pragma unroll
+    for (int a = 0; a < NA; ++a) {
+      const float w = wcol[k * ldw + 32 * a];
+      acc[a] = mfma32(w, b, acc[a]);
+      if constexpr (NT) accT[a] = mfma32(w, bt, accT[a]);
+    }
   }
 }
 
-// ---------------------------------------------------------------------------------------------------
-// node GEMM: Y[n][0:NOUT] = act([X1 | X2][n] W + b) (+ resid[n]); tangent rows RP+n share the A fragments
-// and get no bias, act'(pre) * (X_T W).
-// ---------------------------------------------------------------------------------------------------
-template <int NT>
-__device__ __forceinline__ void node_gemm(const float* X1, int ldx1, int K1, const float* X2, int ldx2, int K2,
+template <int NT, int NA>
+__device__ __forceinline__ void node_task(const float* X1, int ldx1, int K1, const float* X2, int ldx2, int K2,
                                           const float* __restrict__ W, int ldw, const float* __restrict__ bias,
-                                          int NOUT, bool act, const float* resid, int ldr, float* Y, int ldy,
-                                          int RP, int nvalid, int wave, int lane) {
+                                          bool act, const float* resid, int ldr, float* Y, int ldy, int RP,
+                                          int nvalid, int jb, int ct, int lane) {
   const int kk = lane >> 5, li = lane & 31;
-  const int njb = NOUT >> 5, nct = RP >> 5;
-  for (int task = wave; task < njb * nct; task += kWaves) {
-    const int jb = task % njb, ct = task / njb;
-    const int n = ct * 32 + li;
-    f32x16 acc, accT;
-    init_bias(acc, bias, jb, kk);
+  const int n = ct * 32 + li;
+  f32x16 acc[NA], accT[NA];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) accT[r] = 0.f;
-    const gfloat_p wcol = gptr(W) + kk * ldw + jb * 32 + li;
-    node_kloop<NT>(acc, accT, wcol, ldw, X1 + n * ldx1 + kk, X1 + (RP + n) * ldx1 + kk, K1);
-    if (K2 > 0) node_kloop<NT>(acc, accT, wcol + K1 * ldw, ldw, X2 + n * ldx2 + kk, X2 + (RP + n) * ldx2 + kk, K2);
-    if (n < nvalid) {
+  for (int a = 0; a < NA; ++a) {
+    init_bias(acc[a], bias, jb + a, kk);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) accT[a][r] = 0.f;
+  }
+  const gfloat_p wcol = gptr(W) + kk * ldw + jb * 32 + li;
+  node_kloop<NT, NA>(acc, accT, wcol, ldw, X1 + n * ldx1 + kk, X1 + (RP + n) * ldx1 + kk, K1);
+  if (K2 > 0)
+    node_kloop<NT, NA>(acc, accT, wcol + K1 * ldw, ldw, X2 + n * ldx2 + kk, X2 + (RP + n) * ldx2 + kk, K2);
+  if (n < nvalid) {
+#pragma unroll
+    for (int a = 0; a < NA; ++a)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int j = jb * 32 + acc_row(r, kk);
-        float y = acc[r], yT = 0.f;
+        const int j = (jb + a) * 32 + acc_row(r, kk);
+        float y = acc[a][r], yT = 0.f;
         if (act) {
-          silu_dual<NT>(acc[r], NT ? accT[r] : 0.f, y, yT);
+          silu_dual<NT>(acc[a][r], NT ? accT[a][r] : 0.f, y, yT);
         } else if constexpr (NT) {
-          yT = accT[r];
+          yT = accT[a][r];
         }
         if (resid) {
           y += resid[n * ldr + j];
@@ -297,7 +310,29 @@ __device__ __forceinline__ void node_gemm(const float* X1, int ldx1, int K1, con
         Y[n * ldy + j] = y;
         if constexpr (NT) Y[(RP + n) * ldy + j] = yT;
       }
-    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------------
+// node GEMM: Y[n][0:NOUT] = act([X1 | X2][n] W + b) (+ resid[n]); tangent rows RP+n share the A fragments
+// and get no bias, act'(pre) * (X_T W).  Output blocks are paired (shared B reads, two independent MFMA
+// chains) whenever the pairs still give every wave a task.
+// ---------------------------------------------------------------------------------------------------
+template <int NT>
+__device__ __forceinline__ void node_gemm(const float* X1, int ldx1, int K1, const float* X2, int ldx2, int K2,
+                                          const float* __restrict__ W, int ldw, const float* __restrict__ bias,
+                                          int NOUT, bool act, const float* resid, int ldr, float* Y, int ldy,
+                                          int RP, int nvalid, int wave, int lane) {
+  const int njb = NOUT >> 5, nct = RP >> 5;
+  if (false && (njb % 2) == 0 && (njb / 2) * nct >= kWaves) {   // pairing measured slower for phi_h (r01)
+    const int npair = njb / 2;
+    for (int task = wave; task < npair * nct; task += kWaves)
+      node_task<NT, 2>(X1, ldx1, K1, X2, ldx2, K2, W, ldw, bias, act, resid, ldr, Y, ldy, RP, nvalid,
+                       2 * (task % npair), task / npair, lane);
+  } else {
+    for (int task = wave; task < njb * nct; task += kWaves)
+      node_task<NT, 1>(X1, ldx1, K1, X2, ldx2, K2, W, ldw, bias, act, resid, ldr, Y, ldy, RP, nvalid,
+                       task % njb, task / njb, lane);
   }
 }
 
@@ -306,69 +341,168 @@ __device__ __forceinline__ void node_gemm(const float* X1, int ldx1, int K1, con
 // The A fragments of one (output block jb, input block fb) group are 4 dwordx4 per lane (16 MFMAs); groups are
 // software-pipelined PF groups ahead so the L2 latency hides behind MFMAs (counted vmcnt, no vmcnt(0) stalls).
 // ---------------------------------------------------------------------------------------------------
+#ifndef ECNF_EXP_PF
+#define ECNF_EXP_PF 2
+#endif
 template <int NF, int NT>
-__device__ __forceinline__ void chain_layer(const f32x16 (&a)[NF], const f32x16 (&aT)[NF], f32x16 (&b)[NF],
-                                            f32x16 (&bT)[NF], const float* __restrict__ Wpk,
-                                            const float* __restrict__ bias, int lane) {
-  constexpr int NG = NF * NF;           // weight groups per layer
-  constexpr int PF = NT ? 1 : 2;        // groups in flight ahead of the MFMAs
-  const int kk = lane >> 5;
-  const gf32x4_p wp = gptr4(Wpk) + lane;
-  f32x4 wbuf[PF + 1][4];
+__device__ __forceinline__ void chain_epilogue(const f32x16& acc, const f32x16& accT, const f32x4 (&bias)[4],
+                                               f32x16& b, f32x16& bT) {
 #pragma unroll
-  for (int g = 0; g < PF && g < NG; ++g)
+  for (int r = 0; r < 16; ++r) {
+    float y, yT = 0.f;
+#ifdef ECNF_EXP_NO_SILU
+    y = acc[r] + bias[r >> 2][r & 3];   // timing experiment only: wrong numerics
+    yT = NT ? accT[r] : 0.f;
+#else
+    silu_dual<NT>(acc[r] + bias[r >> 2][r & 3], NT ? accT[r] : 0.f, y, yT);   // Dense: x W, then + b
+#endif
+    b[r] = y;
+    if constexpr (NT) bT[r] = yT;
+  }
+}
+
+// SiLU of one slice (NSL slices in all) of a finished output-block pair: value v = 16 h + r of the pair
+template <int NF, int NT, int NSL>
+__device__ __forceinline__ void chain_epilogue_slice(const f32x16 (&acc)[2], const f32x16 (&accT)[2],
+                                                     const f32x4 (&bias)[2][4], f32x16& b0, f32x16& b1,
+                                                     f32x16& bT0, f32x16& bT1, int slice) {
+  constexpr int PER = 32 / NSL;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) wbuf[g][q] = wp[(g * 4 + q) * 64];
-  f32x16 acc, accT;
-#pragma unroll
-  for (int g = 0; g < NG; ++g) {
-    const int jb = g / NF, fb = g % NF;
-    if (g + PF < NG) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) wbuf[(g + PF) % (PF + 1)][q] = wp[((g + PF) * 4 + q) * 64];
-    }
-    if (fb == 0) {
-      init_bias(acc, bias, jb, kk);
-      if constexpr (NT) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) accT[r] = 0.f;
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const f32x4 w = wbuf[g % (PF + 1)][q];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        acc = mfma32(w[e], a[fb][4 * q + e], acc);
-        if constexpr (NT) accT = mfma32(w[e], aT[fb][4 * q + e], accT);
-      }
-    }
-    if (fb == NF - 1) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        float y, yT = 0.f;
-        silu_dual<NT>(acc[r], NT ? accT[r] : 0.f, y, yT);
-        b[jb][r] = y;
-        if constexpr (NT) bT[jb][r] = yT;
-      }
+  for (int i = 0; i < PER; ++i) {
+    const int v = slice * PER + i, h = v >> 4, r = v & 15;
+    float y, yT = 0.f;
+#ifdef ECNF_EXP_NO_SILU
+    y = acc[h][r] + bias[h][r >> 2][r & 3];
+    yT = NT ? accT[h][r] : 0.f;
+#else
+    silu_dual<NT>(acc[h][r] + bias[h][r >> 2][r & 3], NT ? accT[h][r] : 0.f, y, yT);
+#endif
+    if (h == 0) {
+      b0[r] = y;
+      if constexpr (NT) bT0[r] = yT;
+    } else {
+      b1[r] = y;
+      if constexpr (NT) bT1[r] = yT;
     }
   }
 }
 
-template <int NF, int NT, int NL>
-struct Chain {
-  // runs NL layers starting from `a`; the result ends in `a` if NL is even, else in `b`
-  __device__ __forceinline__ static void run(f32x16 (&a)[NF], f32x16 (&aT)[NF], f32x16 (&b)[NF], f32x16 (&bT)[NF],
-                                             const float* Wpk, const float* bias, int lane) {
-    chain_layer<NF, NT>(a, aT, b, bT, Wpk, bias, lane);
-    Chain<NF, NT, NL - 1>::run(b, bT, a, aT, Wpk + NF * NF * 1024, bias + NF * 32, lane);
+// One software pipeline over NL consecutive chain layers (phi_e 2..L, or phi_x 1..L): X[(S+l) & 1] -> X[(S+l+1) & 1],
+// silu(X W + b).  Output blocks go in pairs (jb = 2p, 2p + 1) so every B operand (an input activation register)
+// feeds two independent accumulators.  The weight stream is contiguous across the segment's layers, so the
+// PF-deep group prefetch runs straight across layer boundaries, and the SiLU of each finished pair is deferred
+// into the MFMA region of the next group (also across a layer boundary: the next layer needs block pair 0
+// first, long finished).  Only the segment's very last pair has its SiLU after the final MFMA.
+template <int NF, int NT, int NL, int S>
+__device__ __forceinline__ void chain_segment(f32x16 (&X)[2][NF], f32x16 (&XT)[2][NF],
+                                              const float* __restrict__ Wpk, const float* __restrict__ bias /*LDS*/,
+                                              int lane) {
+  static_assert(NF % 2 == 0, "output blocks are processed in pairs");
+  constexpr int NP = NF / 2;              // output block pairs per layer
+  constexpr int GL = NP * NF;             // group-pairs per layer
+  constexpr int G = NL * GL;              // group-pairs in the segment
+  constexpr int PF = NT ? 1 : ECNF_EXP_PF;   // group-pairs in flight ahead of the MFMAs
+  const int kk = lane >> 5;
+  const gf32x4_p wp = gptr4(Wpk) + lane;
+  // group-pair gg = (layer l, pair p, input block fb); its half h = output block 2p + h sits at
+  // wp[((l * NF * NF + (2p + h) * NF + fb) * 4 + q) * 64]
+  auto gidx = [](int gg, int h) {
+    const int l = gg / GL, g = gg % GL, p = g / NF, fb = g % NF;
+#ifdef ECNF_EXP_ONE_LAYER
+    return ((2 * p + h) * NF + fb) * 4;   // timing experiment: every layer streams layer 0's weights
+#else
+    return (l * NF * NF + (2 * p + h) * NF + fb) * 4;
+#endif
+  };
+  f32x4 wbuf[PF + 1][2][4];
+#pragma unroll
+  for (int gg = 0; gg < PF && gg < G; ++gg)
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) wbuf[gg][h][q] = wp[(gidx(gg, h) + q) * 64];
+  f32x16 acc[2][2], accT[2][2];           // [pair-count parity][h]
+  f32x4 bb[2][2][4];
+#pragma unroll
+  for (int gg = 0; gg < G; ++gg) {
+    const int l = gg / GL, g = gg % GL, p = g / NF, fb = g % NF;
+    const int pc = l * NP + p;            // running pair count (parity picks the accumulator set)
+    if (gg + PF < G) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) wbuf[(gg + PF) % (PF + 1)][h][q] = wp[(gidx(gg + PF, h) + q) * 64];
+    }
+    if (fb == NF - 1) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          bb[pc & 1][h][q] = *reinterpret_cast<const f32x4*>(bias + l * (NF * 32) + (2 * p + h) * 32 + 8 * q + 4 * kk);
+    }
+    // keep the prefetch where it is: without this fence the scheduler sinks the loads to ~4 MFMAs before
+    // their use (register pressure), re-exposing the L2 latency
+#ifndef ECNF_EXP_NO_SCHED_BARRIER
+    __builtin_amdgcn_sched_barrier(0);
+#endif
+    if (fb == 0) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          acc[pc & 1][h][r] = 0.f;
+          if constexpr (NT) accT[pc & 1][h][r] = 0.f;
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float x = X[(S + l) & 1][fb][4 * q + e];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) acc[pc & 1][h] = mfma32(wbuf[gg % (PF + 1)][h][q][e], x, acc[pc & 1][h]);
+        if constexpr (NT) {
+          const float xT = XT[(S + l) & 1][fb][4 * q + e];
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+            accT[pc & 1][h] = mfma32(wbuf[gg % (PF + 1)][h][q][e], xT, accT[pc & 1][h]);
+        }
+      }
+    }
+    // deferred SiLU of the previously finished pair (pair count pc - 1), now that its MFMAs are long issued.
+    // With a single pair per layer (NF == 2) that pair IS the next layer's input block 0, so it cannot wait.
+    if (NP == 1 && fb == NF - 1) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        chain_epilogue<NF, NT>(acc[pc & 1][h], accT[pc & 1][h], bb[pc & 1][h], X[(S + l + 1) & 1][h],
+                               XT[(S + l + 1) & 1][h]);
+    }
+    // Spread over this pair's groups so every MFMA gap carries a few VALU ops instead of a burst.  A layer's
+    // last pair feeds the next layer's blocks 2(NP-1).. , which are read from group fb = 2(NP-1) on, so its
+    // SiLU must finish within the first NSL_LAST groups.
+    if (NP > 1 && pc > 0) {
+      const int lp = (pc - 1) / NP, pp = (pc - 1) % NP;
+      constexpr int NSL_LAST = (2 * (NP - 1)) >= 4 ? 4 : 2;
+      const int nsl = (pp == NP - 1) ? NSL_LAST : (NF >= 4 ? 4 : 2);
+      if (fb < nsl) {
+        if (nsl == 4)
+          chain_epilogue_slice<NF, NT, 4>(acc[(pc - 1) & 1], accT[(pc - 1) & 1], bb[(pc - 1) & 1],
+                                          X[(S + lp + 1) & 1][2 * pp], X[(S + lp + 1) & 1][2 * pp + 1],
+                                          XT[(S + lp + 1) & 1][2 * pp], XT[(S + lp + 1) & 1][2 * pp + 1], fb);
+        else
+          chain_epilogue_slice<NF, NT, 2>(acc[(pc - 1) & 1], accT[(pc - 1) & 1], bb[(pc - 1) & 1],
+                                          X[(S + lp + 1) & 1][2 * pp], X[(S + lp + 1) & 1][2 * pp + 1],
+                                          XT[(S + lp + 1) & 1][2 * pp], XT[(S + lp + 1) & 1][2 * pp + 1], fb);
+      }
+    }
   }
-};
-template <int NF, int NT>
-struct Chain<NF, NT, 0> {
-  __device__ __forceinline__ static void run(f32x16 (&)[NF], f32x16 (&)[NF], f32x16 (&)[NF], f32x16 (&)[NF],
-                                             const float*, const float*, int) {}
-};
+  constexpr int last = NL * NP - 1;
+  if constexpr (NP > 1)
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+    chain_epilogue<NF, NT>(acc[last & 1][h], accT[last & 1][h], bb[last & 1][h], X[(S + NL) & 1][2 * (NP - 1) + h],
+                           XT[(S + NL) & 1][2 * (NP - 1) + h]);
+}
 
 // Segmented (by receiver row) inclusive PREFIX sum over the 32 edge lanes of each half-wave, in DPP:
 // row_shr:1,2,4,8 inside each 16-lane row, then row_bcast:15 carries lane 15's running sum into lanes 16..31
@@ -420,7 +554,7 @@ __device__ __forceinline__ void lds_add(float* p, float v) {
 
 // phi_x output Dense(1) (egnn.py:83-85), shifts_ij = phi_x * r_ij / (C + |r_ij|) and their segment sum
 // (egnn.py:87-94)
-template <int NF, int NT, int D>
+template <int NF, int NT, int L, int D>
 __device__ __forceinline__ void edge_shift(const Net& net, const BlockW& bw, const Lds& s, const f32x16 (&px)[NF],
                                            const f32x16 (&pxT)[NF], bool writer, const SegScan& sc, int rr,
                                            const float (&r)[D], const float (&dr)[D], float length, float dlength,
@@ -431,7 +565,7 @@ __device__ __forceinline__ void edge_shift(const Net& net, const BlockW& bw, con
   for (int fb = 0; fb < NF; ++fb)
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const f32x4 w = gptr4(bw.wx + fb * 32 + 8 * q + 4 * kk)[0];
+      const f32x4 w = *reinterpret_cast<const f32x4*>(s.vecs + (2 * L + 1) * (NF * 32) + fb * 32 + 8 * q + 4 * kk);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         phx += w[e] * px[fb][4 * q + e];
@@ -460,11 +594,12 @@ __device__ __forceinline__ void edge_shift(const Net& net, const BlockW& bw, con
 }
 
 // gate, message aggregation, phi_x torso + output, shifts (egnn.py:81-104); `m` holds the messages
-template <int NF, int NT, int L, int D>
-__device__ __forceinline__ void edge_tail(const Net& net, const BlockW& bw, const Lds& s, f32x16 (&m)[NF],
-                                          f32x16 (&mT)[NF], f32x16 (&o)[NF], f32x16 (&oT)[NF], bool valid,
-                                          int rr, const float (&r)[D], const float (&dr)[D], float length,
-                                          float dlength, int lane) {
+template <int NF, int NT, int L, int D, int MI>
+__device__ __forceinline__ void edge_tail(const Net& net, const BlockW& bw, const Lds& s, f32x16 (&X)[2][NF],
+                                          f32x16 (&XT)[2][NF], bool valid, int rr, const float (&r)[D],
+                                          const float (&dr)[D], float length, float dlength, int lane) {
+  f32x16(&m)[NF] = X[MI];
+  f32x16(&mT)[NF] = XT[MI];
   const int kk = lane >> 5, li = lane & 31;
   // gate e_ij = sigmoid(m_ij . w_g + b_g)  (egnn.py:99-101)
   float part = 0.f, partT = 0.f;
@@ -472,7 +607,7 @@ __device__ __forceinline__ void edge_tail(const Net& net, const BlockW& bw, cons
   for (int fb = 0; fb < NF; ++fb)
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const f32x4 w = gptr4(bw.wg + fb * 32 + 8 * q + 4 * kk)[0];
+      const f32x4 w = *reinterpret_cast<const f32x4*>(s.vecs + (2 * L) * (NF * 32) + fb * 32 + 8 * q + 4 * kk);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         part += w[e] * m[fb][4 * q + e];
@@ -513,14 +648,11 @@ __device__ __forceinline__ void edge_tail(const Net& net, const BlockW& bw, cons
 
   // phi_x torso (egnn.py:82) then its Dense(1) and the shifts
   const float* We = bw.We + (L - 1) * NF * NF * 1024;
-  const float* be = bw.be + (L - 1) * NF * 32;
+  const float* be = s.vecs + (L - 1) * NF * 32;
   We = launder_uniform(We);
-  Chain<NF, NT, L>::run(m, mT, o, oT, We, be, lane);
-  if constexpr (L % 2 == 0) {
-    edge_shift<NF, NT, D>(net, bw, s, m, mT, writer, sc, rr, r, dr, length, dlength, lane);
-  } else {
-    edge_shift<NF, NT, D>(net, bw, s, o, oT, writer, sc, rr, r, dr, length, dlength, lane);
-  }
+  chain_segment<NF, NT, L, MI>(X, XT, We, be, lane);
+  edge_shift<NF, NT, L, D>(net, bw, s, X[(MI + L) & 1], XT[(MI + L) & 1], writer, sc, rr, r, dr, length, dlength,
+                           lane);
 }
 
 // one 32-edge tile through phi_e / gate / phi_x  (egnn.py:72-95)
@@ -570,7 +702,7 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
   }
 
   // phi_e layer 1 from the per-node halves: pre = P_s[s] + P_r[r] + |r|^2 w_d  (egnn.py:76,79)
-  f32x16 X0[NF], X1[NF], T0[NF], T1[NF];
+  f32x16 X[2][NF], XT[2][NF];
   const float* Ps = s.P + rs * s.ld_P;
   const float* Pr = s.P + rr * s.ld_P + M;
   const float* PsT = s.P + (RP + rs) * s.ld_P;
@@ -579,7 +711,7 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
   for (int fb = 0; fb < NF; ++fb)
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const f32x4 w = gptr4(bw.wd + fb * 32 + 8 * q + 4 * kk)[0];
+      const f32x4 w = *reinterpret_cast<const f32x4*>(s.vecs + (2 * L - 1) * (NF * 32) + fb * 32 + 8 * q + 4 * kk);
 #pragma unroll
       for (int e4 = 0; e4 < 4; ++e4) {
         const int row = fb * 32 + 8 * q + 4 * kk + e4;
@@ -588,24 +720,20 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
         if constexpr (NT) {
           const float pT = PsT[row] + PrT[row] + dlen2 * w[e4];
           silu_dual<NT>(p, pT, y, yT);
-          T0[fb][4 * q + e4] = yT;
+          XT[0][fb][4 * q + e4] = yT;
         } else {
           silu_dual<NT>(p, 0.f, y, yT);
         }
-        X0[fb][4 * q + e4] = y;
+        X[0][fb][4 * q + e4] = y;
       }
     }
   STAMP_LANE0(s, kStEdgeLayer1, t_sub);
   // phi_e layers 2..L.  The weight pointer is laundered through an empty asm so the (tile-invariant) weight
   // loads are not hoisted out of the tile loop into thousands of live registers.
   const float* We = launder_uniform(bw.We);
-  Chain<NF, NT, L - 1>::run(X0, T0, X1, T1, We, bw.be, lane);
+  chain_segment<NF, NT, L - 1, 0>(X, XT, We, s.vecs, lane);
   STAMP_LANE0(s, kStEdgeChainE, t_sub);
-  if constexpr ((L - 1) % 2 == 0) {
-    edge_tail<NF, NT, L, D>(net, bw, s, X0, T0, X1, T1, valid, rr, r, dr, length, dlength, lane);
-  } else {
-    edge_tail<NF, NT, L, D>(net, bw, s, X1, T1, X0, T0, valid, rr, r, dr, length, dlength, lane);
-  }
+  edge_tail<NF, NT, L, D, (L - 1) & 1>(net, bw, s, X, XT, valid, rr, r, dr, length, dlength, lane);
   STAMP_LANE0(s, kStEdgeTail, t_sub);
 }
 
@@ -660,6 +788,16 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
   const int ntiles = (MPW * net.EP) >> 5;
   for (int k = 0; k < net.K; ++k) {
     const BlockW& bw = net.blk[k];
+    // stage this block's chain biases and the w_d / w_g / w_x vectors in LDS (read by every edge tile)
+    for (int idx = tid; idx < (2 * L + 2) * M; idx += kThreads) {
+      const int v = idx / M, c = idx - v * M;
+      float val;
+      if (v < 2 * L - 1) val = gptr(bw.be)[idx];
+      else if (v == 2 * L - 1) val = gptr(bw.wd)[c];
+      else if (v == 2 * L) val = gptr(bw.wg)[c];
+      else val = gptr(bw.wx)[c];
+      s.vecs[idx] = val;
+    }
     // h <- Dense([h | temb])  (egnn.py:166-167)
     node_gemm<NT>(s.hin, s.ld_hin, H + T, nullptr, 0, 0, bw.Wn, H, bw.bn, H, false, nullptr, 0, s.hb, s.ld_hb, RP,
                   nvalid, wave, lane);

@@ -7,7 +7,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "ecnf-baseline-neurips-2023_amd"))
-os.environ["ECNF_LIB"] = os.path.join(ROOT, "tools", "libecnf_hip_stamps.so")
+os.environ["ECNF_LIB"] = os.environ.get("ECNF_STAMPS_LIB", os.path.join(ROOT, "tools", "libecnf_hip_stamps.so"))
 
 import torch  # noqa: E402
 from ecnf_amd import CONFIGS, init_params, _lib  # noqa: E402
