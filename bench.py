@@ -66,6 +66,7 @@ def main():
     ap.add_argument("--nfe", type=int, default=100)
     ap.add_argument("--cpu-molecules", type=int, default=160, help="bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "0") or 0))
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL over xGMI) or gloo (multi-rank rehearsal)")
     args = ap.parse_args()
 
     import numpy as np
@@ -77,9 +78,14 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    ndev = max(1, torch.cuda.device_count())
+    local = local % ndev                      # one rank per GPU; folds ranks onto fewer GPUs only in rehearsals
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(args.dist_backend)
     dev = torch.device("cuda", local)
     cfg = CONFIGS[args.config]
 
@@ -113,7 +119,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+    t = torch.tensor([elapsed], device=dev if args.dist_backend == "nccl" else "cpu", dtype=torch.float64)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     t_max = float(t.item())
