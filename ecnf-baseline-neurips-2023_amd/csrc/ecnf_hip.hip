@@ -81,6 +81,7 @@ __device__ inline float clip_end(float tn, float tau1) { return tn > tau1 - 1e-6
 template <int NF, int NT, int L, int D>
 __device__ __forceinline__ void joint_field(const Net& net, const Lds& s, const SolverLds& st, const SolveP& sp,
                                             float* kx_out, float* kl_out) {
+  constexpr int kThreads = Geo<NT>::NTHR;
   const int tid = threadIdx.x, MPW = net.MPW, ND = net.ND;
   // NT == 0: one primal eval; Hutchinson: one JVP along eps; exact: ND JVPs along e_k (trace of J)
   const int nrep = (NT == 0 || sp.div == ECNF_DIV_HUTCHINSON) ? 1 : ND;
@@ -125,11 +126,12 @@ enum Phase { kEuler = 0, kInit0 = 1, kInit1 = 2, kFsal = 3, kStage = 4 };
 
 // The whole solve as a phase machine around ONE field evaluation per loop trip.
 template <int NF, int NT, int L, int D>
-__global__ __launch_bounds__(kThreads) void integrate_kernel(Net net, SolveP sp, const float* __restrict__ y0,
-                                                             const int32_t* __restrict__ feat,
-                                                             const float* __restrict__ eps, float* y1,
-                                                             float* dlogp, int32_t* nfe_out, int32_t* status_out,
-                                                             int B) {
+__global__ __launch_bounds__(Geo<NT>::NTHR) void integrate_kernel(Net net, SolveP sp, const float* __restrict__ y0,
+                                                                  const int32_t* __restrict__ feat,
+                                                                  const float* __restrict__ eps, float* y1,
+                                                                  float* dlogp, int32_t* nfe_out,
+                                                                  int32_t* status_out, int B) {
+  constexpr int kThreads = Geo<NT>::NTHR;
   extern __shared__ float smem[];
   const int tid = threadIdx.x, MPW = net.MPW, ND = net.ND, N = net.N;
   const Lds s = carve_lds<NT>(net, smem);
@@ -361,10 +363,12 @@ __global__ __launch_bounds__(kThreads) void integrate_kernel(Net net, SolveP sp,
 
 // one evaluation (and n_tangents JVPs) per molecule
 template <int NF, int NT, int L, int D>
-__global__ __launch_bounds__(kThreads) void vf_kernel(Net net, const float* __restrict__ x, const float* __restrict__ t,
-                                                      const int32_t* __restrict__ feat,
-                                                      const float* __restrict__ tan_in, int ntan, float* v,
-                                                      float* tan_out, int B) {
+__global__ __launch_bounds__(Geo<NT>::NTHR) void vf_kernel(Net net, const float* __restrict__ x,
+                                                           const float* __restrict__ t,
+                                                           const int32_t* __restrict__ feat,
+                                                           const float* __restrict__ tan_in, int ntan, float* v,
+                                                           float* tan_out, int B) {
+  constexpr int kThreads = Geo<NT>::NTHR;
   extern __shared__ float smem[];
   const int tid = threadIdx.x, MPW = net.MPW, ND = net.ND, N = net.N;
   const Lds s = carve_lds<NT>(net, smem);
@@ -528,7 +532,7 @@ int choose_mpw(const ecnf_cfg& c, int NT, int* mpw_out, size_t* lds_out, int* rp
     if (bytes > 160 * 1024) break;
     const int EP = 32 * ((E + 31) / 32);
     const int tiles = m * EP / 32;
-    const double eff = (double)tiles / (kWaves * ((tiles + kWaves - 1) / kWaves)) * (double)(m * E) / (tiles * 32.0);
+    const double eff = (double)tiles / (kSimds * ((tiles + kSimds - 1) / kSimds)) * (double)(m * E) / (tiles * 32.0);
     if (forced ? m == forced : eff > best + 1e-9) {
       best = eff;
       best_m = m;
@@ -553,7 +557,7 @@ hipError_t launch_integrate(const ecnf_handle* h, const SolveP& sp, const float*
   hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds[NT]);
   if (e != hipSuccess) return e;
   const int grid = (B + h->net[NT].MPW - 1) / h->net[NT].MPW;
-  hipLaunchKernelGGL(k, dim3(grid), dim3(kThreads), h->lds[NT], stream, h->net[NT], sp, y0, feat, eps, y1, dlogp,
+  hipLaunchKernelGGL(k, dim3(grid), dim3(Geo<NT>::NTHR), h->lds[NT], stream, h->net[NT], sp, y0, feat, eps, y1, dlogp,
                      nfe, status, B);
   return hipGetLastError();
 }
@@ -565,7 +569,7 @@ hipError_t launch_vf(const ecnf_handle* h, const float* x, const float* t, const
   hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds[NT]);
   if (e != hipSuccess) return e;
   const int grid = (B + h->net[NT].MPW - 1) / h->net[NT].MPW;
-  hipLaunchKernelGGL(k, dim3(grid), dim3(kThreads), h->lds[NT], stream, h->net[NT], x, t, feat, tan_in, ntan, v,
+  hipLaunchKernelGGL(k, dim3(grid), dim3(Geo<NT>::NTHR), h->lds[NT], stream, h->net[NT], x, t, feat, tan_in, ntan, v,
                      tan_out, B);
   return hipGetLastError();
 }

@@ -4,7 +4,7 @@
 // and EGCL.__call__ (ecnf/nets/egnn.py:49-114) of the reference, with forward-mode tangents (NT = 1) for the
 // divergence terms of ecnf/cnf/sample_and_log_prob.py:57-78.
 //
-// Layout (per workgroup = 4 waves = 256 threads, MPW molecules):
+// Layout (per workgroup = Geo<NT>::NW waves, MPW molecules):
 //   * node rows: molecule m, atom i -> row n = m*N + i, padded to RP = 32*ceil(MPW*N/32); tangent row of n is
 //     RP + n.  All node state lives in LDS as [row][feature] with odd leading dimensions (conflict-free
 //     column reads by 32 lanes).
@@ -25,16 +25,38 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+#include <utility>
+
 namespace ecnf {
 
-constexpr int kWaves = 4;
-constexpr int kThreads = 64 * kWaves;
+constexpr int kSimds = 4;   // SIMDs per CU
+// Waves per workgroup: the primal kernels run 8 waves = 2 per SIMD (<= 256 registers each), so one wave's VALU
+// work (SiLU, scans) overlaps the other wave's fp32 MFMA stream (measured: a co-resident VALU wave leaves the
+// MFMA wave at 64 cycles/MFMA, while VALU issued between a wave's OWN MFMAs adds ~5-11 cycles each).  The tangent
+// kernels carry twice the activations and keep 4 waves (1 per SIMD).
+template <int NT>
+struct Geo {
+  static constexpr int NW = NT ? 4 : 8;
+  static constexpr int NTHR = 64 * NW;
+};
 constexpr int kMaxBlocks = 10;
 constexpr int kMaxPhiH = 5;     // L + 1 <= 5
 constexpr int kMaxHalfT = 8;    // T <= 16
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// compile-time loop: f(std::integral_constant<int, i>) for i = 0..N-1, always fully expanded (a long unrolled
+// loop that the optimiser only partially unrolls turns ring-buffer register indices dynamic -> scratch)
+template <typename F, int... I>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
 
 // global (address space 1) views of the weight buffers: global_load_* with counted vmcnt waits instead of flat
 // loads, which hipcc must fence with vmcnt(0) lgkmcnt(0)
@@ -318,19 +340,19 @@ __device__ __forceinline__ void node_task(const float* X1, int ldx1, int K1, con
 // and get no bias, act'(pre) * (X_T W).  Output blocks are paired (shared B reads, two independent MFMA
 // chains) whenever the pairs still give every wave a task.
 // ---------------------------------------------------------------------------------------------------
-template <int NT>
+template <int NT, int NW>
 __device__ __forceinline__ void node_gemm(const float* X1, int ldx1, int K1, const float* X2, int ldx2, int K2,
                                           const float* __restrict__ W, int ldw, const float* __restrict__ bias,
                                           int NOUT, bool act, const float* resid, int ldr, float* Y, int ldy,
                                           int RP, int nvalid, int wave, int lane) {
   const int njb = NOUT >> 5, nct = RP >> 5;
-  if (false && (njb % 2) == 0 && (njb / 2) * nct >= kWaves) {   // pairing measured slower for phi_h (r01)
+  if (false && (njb % 2) == 0 && (njb / 2) * nct >= NW) {   // pairing measured slower for phi_h (r01)
     const int npair = njb / 2;
-    for (int task = wave; task < npair * nct; task += kWaves)
+    for (int task = wave; task < npair * nct; task += NW)
       node_task<NT, 2>(X1, ldx1, K1, X2, ldx2, K2, W, ldw, bias, act, resid, ldr, Y, ldy, RP, nvalid,
                        2 * (task % npair), task / npair, lane);
   } else {
-    for (int task = wave; task < njb * nct; task += kWaves)
+    for (int task = wave; task < njb * nct; task += NW)
       node_task<NT, 1>(X1, ldx1, K1, X2, ldx2, K2, W, ldw, bias, act, resid, ldr, Y, ldy, RP, nvalid,
                        task % njb, task / njb, lane);
   }
@@ -342,166 +364,83 @@ __device__ __forceinline__ void node_gemm(const float* X1, int ldx1, int K1, con
 // software-pipelined PF groups ahead so the L2 latency hides behind MFMAs (counted vmcnt, no vmcnt(0) stalls).
 // ---------------------------------------------------------------------------------------------------
 #ifndef ECNF_EXP_PF
-#define ECNF_EXP_PF 2
+#define ECNF_EXP_PF 1
 #endif
-template <int NF, int NT>
-__device__ __forceinline__ void chain_epilogue(const f32x16& acc, const f32x16& accT, const f32x4 (&bias)[4],
-                                               f32x16& b, f32x16& bT) {
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    float y, yT = 0.f;
-#ifdef ECNF_EXP_NO_SILU
-    y = acc[r] + bias[r >> 2][r & 3];   // timing experiment only: wrong numerics
-    yT = NT ? accT[r] : 0.f;
-#else
-    silu_dual<NT>(acc[r] + bias[r >> 2][r & 3], NT ? accT[r] : 0.f, y, yT);   // Dense: x W, then + b
-#endif
-    b[r] = y;
-    if constexpr (NT) bT[r] = yT;
-  }
-}
-
-// SiLU of one slice (NSL slices in all) of a finished output-block pair: value v = 16 h + r of the pair
-template <int NF, int NT, int NSL>
-__device__ __forceinline__ void chain_epilogue_slice(const f32x16 (&acc)[2], const f32x16 (&accT)[2],
-                                                     const f32x4 (&bias)[2][4], f32x16& b0, f32x16& b1,
-                                                     f32x16& bT0, f32x16& bT1, int slice) {
-  constexpr int PER = 32 / NSL;
-#pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    const int v = slice * PER + i, h = v >> 4, r = v & 15;
-    float y, yT = 0.f;
-#ifdef ECNF_EXP_NO_SILU
-    y = acc[h][r] + bias[h][r >> 2][r & 3];
-    yT = NT ? accT[h][r] : 0.f;
-#else
-    silu_dual<NT>(acc[h][r] + bias[h][r >> 2][r & 3], NT ? accT[h][r] : 0.f, y, yT);
-#endif
-    if (h == 0) {
-      b0[r] = y;
-      if constexpr (NT) bT0[r] = yT;
-    } else {
-      b1[r] = y;
-      if constexpr (NT) bT1[r] = yT;
-    }
-  }
-}
-
-// One software pipeline over NL consecutive chain layers (phi_e 2..L, or phi_x 1..L): X[(S+l) & 1] -> X[(S+l+1) & 1],
-// silu(X W + b).  Output blocks go in pairs (jb = 2p, 2p + 1) so every B operand (an input activation register)
-// feeds two independent accumulators.  The weight stream is contiguous across the segment's layers, so the
-// PF-deep group prefetch runs straight across layer boundaries, and the SiLU of each finished pair is deferred
-// into the MFMA region of the next group (also across a layer boundary: the next layer needs block pair 0
-// first, long finished).  Only the segment's very last pair has its SiLU after the final MFMA.
-template <int NF, int NT, int NL, int S>
-__device__ __forceinline__ void chain_segment(f32x16 (&X)[2][NF], f32x16 (&XT)[2][NF],
-                                              const float* __restrict__ Wpk, const float* __restrict__ bias /*LDS*/,
-                                              int lane) {
-  static_assert(NF % 2 == 0, "output blocks are processed in pairs");
-  constexpr int NP = NF / 2;              // output block pairs per layer
-  constexpr int GL = NP * NF;             // group-pairs per layer
-  constexpr int G = NL * GL;              // group-pairs in the segment
-  constexpr int PF = NT ? 1 : ECNF_EXP_PF;   // group-pairs in flight ahead of the MFMAs
+// One software pipeline over NL consecutive chain layers (phi_e 2..L, or phi_x 1..L), IN PLACE:
+// X <- silu(X W_l + b_l) for l = 0..NL-1.  Per layer the NF output blocks accumulate side by side (fb-major
+// group order: consecutive MFMAs hit different accumulators) and the SiLU of all blocks overwrites the input
+// once its last MFMA has issued, so a wave holds 16 NF activation + 16 NF accumulator registers (<= 256 total
+// at NF = 4: two waves per SIMD).  The weight stream is contiguous across layers; the PF-group prefetch runs
+// straight over layer boundaries and is pinned by a sched_barrier.
+template <int NF, int NT, int NL>
+__device__ __forceinline__ void chain_segment(f32x16 (&X)[NF], f32x16 (&XT)[NF], const float* __restrict__ Wpk,
+                                              const float* __restrict__ bias /* LDS, [NL][M] */, int lane) {
+  constexpr int GL = NF * NF;             // groups per layer, g = fb * NF + jb
+  constexpr int G = NL * GL;
+  constexpr int PF = ECNF_EXP_PF;         // groups in flight ahead of the MFMAs
   const int kk = lane >> 5;
   const gf32x4_p wp = gptr4(Wpk) + lane;
-  // group-pair gg = (layer l, pair p, input block fb); its half h = output block 2p + h sits at
-  // wp[((l * NF * NF + (2p + h) * NF + fb) * 4 + q) * 64]
-  auto gidx = [](int gg, int h) {
-    const int l = gg / GL, g = gg % GL, p = g / NF, fb = g % NF;
-#ifdef ECNF_EXP_ONE_LAYER
-    return ((2 * p + h) * NF + fb) * 4;   // timing experiment: every layer streams layer 0's weights
-#else
-    return (l * NF * NF + (2 * p + h) * NF + fb) * 4;
-#endif
+  // group (l, jb, fb) sits at wp[((l * NF * NF + jb * NF + fb) * 4 + q) * 64]
+  auto gidx = [](int gg) constexpr {
+    const int l = gg / GL, g = gg % GL, fb = g / NF, jb = g % NF;
+    return (l * NF * NF + jb * NF + fb) * 4;
   };
-  f32x4 wbuf[PF + 1][2][4];
+  f32x4 wbuf[PF + 1][4];
 #pragma unroll
   for (int gg = 0; gg < PF && gg < G; ++gg)
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
+    for (int q = 0; q < 4; ++q) wbuf[gg][q] = wp[(gidx(gg) + q) * 64];
+  f32x16 acc[NF], accT[NF];
+  static_for<G>([&](auto GGc) {
+    constexpr int gg = decltype(GGc)::value;
+    constexpr int l = gg / GL, g = gg % GL, fb = g / NF, jb = g % NF;
+    if constexpr (gg + PF < G) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) wbuf[gg][h][q] = wp[(gidx(gg, h) + q) * 64];
-  f32x16 acc[2][2], accT[2][2];           // [pair-count parity][h]
-  f32x4 bb[2][2][4];
-#pragma unroll
-  for (int gg = 0; gg < G; ++gg) {
-    const int l = gg / GL, g = gg % GL, p = g / NF, fb = g % NF;
-    const int pc = l * NP + p;            // running pair count (parity picks the accumulator set)
-    if (gg + PF < G) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) wbuf[(gg + PF) % (PF + 1)][h][q] = wp[(gidx(gg + PF, h) + q) * 64];
+      for (int q = 0; q < 4; ++q) wbuf[(gg + PF) % (PF + 1)][q] = wp[(gidx(gg + PF) + q) * 64];
     }
-    if (fb == NF - 1) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          bb[pc & 1][h][q] = *reinterpret_cast<const f32x4*>(bias + l * (NF * 32) + (2 * p + h) * 32 + 8 * q + 4 * kk);
-    }
-    // keep the prefetch where it is: without this fence the scheduler sinks the loads to ~4 MFMAs before
-    // their use (register pressure), re-exposing the L2 latency
 #ifndef ECNF_EXP_NO_SCHED_BARRIER
     __builtin_amdgcn_sched_barrier(0);
 #endif
-    if (fb == 0) {
+    if constexpr (fb == 0) {
 #pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          acc[pc & 1][h][r] = 0.f;
-          if constexpr (NT) accT[pc & 1][h][r] = 0.f;
-        }
+      for (int r = 0; r < 16; ++r) {
+        acc[jb][r] = 0.f;
+        if constexpr (NT) accT[jb][r] = 0.f;
+      }
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
+      const f32x4 w = wbuf[gg % (PF + 1)][q];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const float x = X[(S + l) & 1][fb][4 * q + e];
+        acc[jb] = mfma32(w[e], X[fb][4 * q + e], acc[jb]);
+        if constexpr (NT) accT[jb] = mfma32(w[e], XT[fb][4 * q + e], accT[jb]);
+      }
+    }
+    if constexpr (g == GL - 1) {
+      // layer complete: X <- silu(acc + b)  (Dense: x W, then + b; mlp.py:14)
 #pragma unroll
-        for (int h = 0; h < 2; ++h) acc[pc & 1][h] = mfma32(wbuf[gg % (PF + 1)][h][q][e], x, acc[pc & 1][h]);
-        if constexpr (NT) {
-          const float xT = XT[(S + l) & 1][fb][4 * q + e];
+      for (int j = 0; j < NF; ++j) {
 #pragma unroll
-          for (int h = 0; h < 2; ++h)
-            accT[pc & 1][h] = mfma32(wbuf[gg % (PF + 1)][h][q][e], xT, accT[pc & 1][h]);
+        for (int q = 0; q < 4; ++q) {
+          const f32x4 b4 = *reinterpret_cast<const f32x4*>(bias + l * (NF * 32) + j * 32 + 8 * q + 4 * kk);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int r = 4 * q + e;
+            float y, yT = 0.f;
+#ifdef ECNF_EXP_NO_SILU
+            y = acc[j][r] + b4[e];
+            yT = NT ? accT[j][r] : 0.f;
+#else
+            silu_dual<NT>(acc[j][r] + b4[e], NT ? accT[j][r] : 0.f, y, yT);
+#endif
+            X[j][r] = y;
+            if constexpr (NT) XT[j][r] = yT;
+          }
         }
       }
     }
-    // deferred SiLU of the previously finished pair (pair count pc - 1), now that its MFMAs are long issued.
-    // With a single pair per layer (NF == 2) that pair IS the next layer's input block 0, so it cannot wait.
-    if (NP == 1 && fb == NF - 1) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-        chain_epilogue<NF, NT>(acc[pc & 1][h], accT[pc & 1][h], bb[pc & 1][h], X[(S + l + 1) & 1][h],
-                               XT[(S + l + 1) & 1][h]);
-    }
-    // Spread over this pair's groups so every MFMA gap carries a few VALU ops instead of a burst.  A layer's
-    // last pair feeds the next layer's blocks 2(NP-1).. , which are read from group fb = 2(NP-1) on, so its
-    // SiLU must finish within the first NSL_LAST groups.
-    if (NP > 1 && pc > 0) {
-      const int lp = (pc - 1) / NP, pp = (pc - 1) % NP;
-      constexpr int NSL_LAST = (2 * (NP - 1)) >= 4 ? 4 : 2;
-      const int nsl = (pp == NP - 1) ? NSL_LAST : (NF >= 4 ? 4 : 2);
-      if (fb < nsl) {
-        if (nsl == 4)
-          chain_epilogue_slice<NF, NT, 4>(acc[(pc - 1) & 1], accT[(pc - 1) & 1], bb[(pc - 1) & 1],
-                                          X[(S + lp + 1) & 1][2 * pp], X[(S + lp + 1) & 1][2 * pp + 1],
-                                          XT[(S + lp + 1) & 1][2 * pp], XT[(S + lp + 1) & 1][2 * pp + 1], fb);
-        else
-          chain_epilogue_slice<NF, NT, 2>(acc[(pc - 1) & 1], accT[(pc - 1) & 1], bb[(pc - 1) & 1],
-                                          X[(S + lp + 1) & 1][2 * pp], X[(S + lp + 1) & 1][2 * pp + 1],
-                                          XT[(S + lp + 1) & 1][2 * pp], XT[(S + lp + 1) & 1][2 * pp + 1], fb);
-      }
-    }
-  }
-  constexpr int last = NL * NP - 1;
-  if constexpr (NP > 1)
-#pragma unroll
-  for (int h = 0; h < 2; ++h)
-    chain_epilogue<NF, NT>(acc[last & 1][h], accT[last & 1][h], bb[last & 1][h], X[(S + NL) & 1][2 * (NP - 1) + h],
-                           XT[(S + NL) & 1][2 * (NP - 1) + h]);
+  });
 }
 
 // Segmented (by receiver row) inclusive PREFIX sum over the 32 edge lanes of each half-wave, in DPP:
@@ -594,12 +533,12 @@ __device__ __forceinline__ void edge_shift(const Net& net, const BlockW& bw, con
 }
 
 // gate, message aggregation, phi_x torso + output, shifts (egnn.py:81-104); `m` holds the messages
-template <int NF, int NT, int L, int D, int MI>
-__device__ __forceinline__ void edge_tail(const Net& net, const BlockW& bw, const Lds& s, f32x16 (&X)[2][NF],
-                                          f32x16 (&XT)[2][NF], bool valid, int rr, const float (&r)[D],
+template <int NF, int NT, int L, int D>
+__device__ __forceinline__ void edge_tail(const Net& net, const BlockW& bw, const Lds& s, f32x16 (&X)[NF],
+                                          f32x16 (&XT)[NF], bool valid, int rr, const float (&r)[D],
                                           const float (&dr)[D], float length, float dlength, int lane) {
-  f32x16(&m)[NF] = X[MI];
-  f32x16(&mT)[NF] = XT[MI];
+  f32x16(&m)[NF] = X;
+  f32x16(&mT)[NF] = XT;
   const int kk = lane >> 5, li = lane & 31;
   // gate e_ij = sigmoid(m_ij . w_g + b_g)  (egnn.py:99-101)
   float part = 0.f, partT = 0.f;
@@ -650,9 +589,8 @@ __device__ __forceinline__ void edge_tail(const Net& net, const BlockW& bw, cons
   const float* We = bw.We + (L - 1) * NF * NF * 1024;
   const float* be = s.vecs + (L - 1) * NF * 32;
   We = launder_uniform(We);
-  chain_segment<NF, NT, L, MI>(X, XT, We, be, lane);
-  edge_shift<NF, NT, L, D>(net, bw, s, X[(MI + L) & 1], XT[(MI + L) & 1], writer, sc, rr, r, dr, length, dlength,
-                           lane);
+  chain_segment<NF, NT, L>(X, XT, We, be, lane);
+  edge_shift<NF, NT, L, D>(net, bw, s, X, XT, writer, sc, rr, r, dr, length, dlength, lane);
 }
 
 // one 32-edge tile through phi_e / gate / phi_x  (egnn.py:72-95)
@@ -702,7 +640,7 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
   }
 
   // phi_e layer 1 from the per-node halves: pre = P_s[s] + P_r[r] + |r|^2 w_d  (egnn.py:76,79)
-  f32x16 X[2][NF], XT[2][NF];
+  f32x16 X[NF], XT[NF];
   const float* Ps = s.P + rs * s.ld_P;
   const float* Pr = s.P + rr * s.ld_P + M;
   const float* PsT = s.P + (RP + rs) * s.ld_P;
@@ -720,20 +658,20 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
         if constexpr (NT) {
           const float pT = PsT[row] + PrT[row] + dlen2 * w[e4];
           silu_dual<NT>(p, pT, y, yT);
-          XT[0][fb][4 * q + e4] = yT;
+          XT[fb][4 * q + e4] = yT;
         } else {
           silu_dual<NT>(p, 0.f, y, yT);
         }
-        X[0][fb][4 * q + e4] = y;
+        X[fb][4 * q + e4] = y;
       }
     }
   STAMP_LANE0(s, kStEdgeLayer1, t_sub);
   // phi_e layers 2..L.  The weight pointer is laundered through an empty asm so the (tile-invariant) weight
   // loads are not hoisted out of the tile loop into thousands of live registers.
   const float* We = launder_uniform(bw.We);
-  chain_segment<NF, NT, L - 1, 0>(X, XT, We, s.vecs, lane);
+  chain_segment<NF, NT, L - 1>(X, XT, We, s.vecs, lane);
   STAMP_LANE0(s, kStEdgeChainE, t_sub);
-  edge_tail<NF, NT, L, D, (L - 1) & 1>(net, bw, s, X, XT, valid, rr, r, dr, length, dlength, lane);
+  edge_tail<NF, NT, L, D>(net, bw, s, X, XT, valid, rr, r, dr, length, dlength, lane);
   STAMP_LANE0(s, kStEdgeTail, t_sub);
 }
 
@@ -744,27 +682,28 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
 template <int NF, int NT, int L, int D>
 __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const float* x_in, const float* t_in, const float* tan_in,
                           float* v_out, float* tan_out) {
+  constexpr int kNW = Geo<NT>::NW, kNT = Geo<NT>::NTHR;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int N = net.N, H = net.H, T = net.T, M = NF * 32, RP = net.RP, MPW = net.MPW, ND = net.ND;
   const int nvalid = MPW * N;
   const int R = RP * (1 + NT);
 
   // ---- prologue: input mean, centring (egnn.py:160), embedding (build_cnf.py:79-83) ----
-  for (int idx = tid; idx < MPW * D * (1 + NT); idx += kThreads) {
+  for (int idx = tid; idx < MPW * D * (1 + NT); idx += kNT) {
     const int which = idx / (MPW * D), md = idx - which * MPW * D, m = md / D, d = md - m * D;
     const float* src = (which == 0 ? x_in : tan_in) + m * ND + d;
     float acc = 0.f;
     for (int i = 0; i < N; ++i) acc += src[i * D];
     s.mean[idx] = acc / (float)N;
   }
-  for (int idx = tid; idx < MPW * T; idx += kThreads) {
+  for (int idx = tid; idx < MPW * T; idx += kNT) {
     const int m = idx / T, k = idx - m * T, half = T >> 1;
     const float ts = t_in[m] * 1000.0f;                   // build_cnf.py:23
     const float arg = ts * net.freqs[k < half ? k : k - half];
     s.temb[idx] = k < half ? sinf(arg) : cosf(arg);
   }
   __syncthreads();
-  for (int idx = tid; idx < nvalid * D * (1 + NT); idx += kThreads) {
+  for (int idx = tid; idx < nvalid * D * (1 + NT); idx += kNT) {
     const int which = idx / (nvalid * D), nd = idx - which * nvalid * D, n = nd / D, d = nd - n * D;
     const int m = n / N;
     const float* src = which == 0 ? x_in : tan_in;
@@ -773,7 +712,7 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
     s.xc[row * D + d] = v;
     s.xc0[row * D + d] = v;
   }
-  for (int idx = tid; idx < R * (H + T); idx += kThreads) {
+  for (int idx = tid; idx < R * (H + T); idx += kNT) {
     const int row = idx / (H + T), c = idx - row * (H + T);
     float v = 0.f;
     if (row < nvalid) {
@@ -789,7 +728,7 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
   for (int k = 0; k < net.K; ++k) {
     const BlockW& bw = net.blk[k];
     // stage this block's chain biases and the w_d / w_g / w_x vectors in LDS (read by every edge tile)
-    for (int idx = tid; idx < (2 * L + 2) * M; idx += kThreads) {
+    for (int idx = tid; idx < (2 * L + 2) * M; idx += kNT) {
       const int v = idx / M, c = idx - v * M;
       float val;
       if (v < 2 * L - 1) val = gptr(bw.be)[idx];
@@ -799,25 +738,26 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
       s.vecs[idx] = val;
     }
     // h <- Dense([h | temb])  (egnn.py:166-167)
-    node_gemm<NT>(s.hin, s.ld_hin, H + T, nullptr, 0, 0, bw.Wn, H, bw.bn, H, false, nullptr, 0, s.hb, s.ld_hb, RP,
+    node_gemm<NT, kNW>(s.hin, s.ld_hin, H + T, nullptr, 0, 0, bw.Wn, H, bw.bn, H, false, nullptr, 0, s.hb, s.ld_hb, RP,
                   nvalid, wave, lane);
     __syncthreads();
     STAMP(s, kStNodeDense);
     // per-node halves of phi_e layer 1
-    node_gemm<NT>(s.hb, s.ld_hb, H, nullptr, 0, 0, bw.Wp, 2 * M, bw.bp, 2 * M, false, nullptr, 0, s.P, s.ld_P, RP,
+    node_gemm<NT, kNW>(s.hb, s.ld_hb, H, nullptr, 0, 0, bw.Wp, 2 * M, bw.bp, 2 * M, false, nullptr, 0, s.P, s.ld_P, RP,
                   nvalid, wave, lane);
     __syncthreads();
     STAMP(s, kStPGemm);
     // edges
-    for (int tile = wave; tile < ntiles; tile += kWaves) edge_tile<NF, NT, L, D>(net, bw, s, tile, lane);
+    // tile t runs on wave t mod NW, i.e. SIMD t mod 4: every SIMD gets ceil/floor(ntiles / 4) tiles
+    for (int tile = wave; tile < ntiles; tile += kNW) edge_tile<NF, NT, L, D>(net, bw, s, tile, lane);
     __syncthreads();
     STAMP(s, kStEdge);
     // node update: x += shift_i / (N-1) (egnn.py:95,113); m_i /= sqrt(N-1) (egnn.py:104)
-    for (int idx = tid; idx < R * D; idx += kThreads) {
+    for (int idx = tid; idx < R * D; idx += kNT) {
       s.xc[idx] += s.dxacc[idx] / net.nn1;
       s.dxacc[idx] = 0.f;
     }
-    for (int idx = tid; idx < R * M; idx += kThreads) {
+    for (int idx = tid; idx < R * M; idx += kNT) {
       const int row = idx / M, c = idx - row * M;
       s.macc[row * s.ld_m + c] /= net.sqrt_nn1;
     }
@@ -826,27 +766,27 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
     // phi_h = MLP((M,)*L + (H,)) on [m_i | h], residual (egnn.py:105-111)
     float* Q0 = s.P;
     float* Q1 = s.P + (M + 1);
-    node_gemm<NT>(s.macc, s.ld_m, M, s.hb, s.ld_hb, H, bw.Wh[0], M, bw.bh[0], M, true, nullptr, 0, Q0, s.ld_P, RP,
+    node_gemm<NT, kNW>(s.macc, s.ld_m, M, s.hb, s.ld_hb, H, bw.Wh[0], M, bw.bh[0], M, true, nullptr, 0, Q0, s.ld_P, RP,
                   nvalid, wave, lane);
     __syncthreads();
-    for (int idx = tid; idx < R * M; idx += kThreads) {
+    for (int idx = tid; idx < R * M; idx += kNT) {
       const int row = idx / M, c = idx - row * M;
       s.macc[row * s.ld_m + c] = 0.f;
     }
     for (int l = 1; l < L; ++l) {
-      node_gemm<NT>(Q0, s.ld_P, M, nullptr, 0, 0, bw.Wh[l], M, bw.bh[l], M, true, nullptr, 0, Q1, s.ld_P, RP,
+      node_gemm<NT, kNW>(Q0, s.ld_P, M, nullptr, 0, 0, bw.Wh[l], M, bw.bh[l], M, true, nullptr, 0, Q1, s.ld_P, RP,
                     nvalid, wave, lane);
       __syncthreads();
       float* tq = Q0; Q0 = Q1; Q1 = tq;
     }
-    node_gemm<NT>(Q0, s.ld_P, M, nullptr, 0, 0, bw.Wh[L], H, bw.bh[L], H, false, s.hb, s.ld_hb, s.hin, s.ld_hin, RP,
+    node_gemm<NT, kNW>(Q0, s.ld_P, M, nullptr, 0, 0, bw.Wh[L], H, bw.bh[L], H, false, s.hb, s.ld_hb, s.hin, s.ld_hin, RP,
                   nvalid, wave, lane);
     __syncthreads();
     STAMP(s, kStPhiH);
   }
 
   // ---- epilogue: v = ((x_K - x_c0) - mean(x_in)) * final_scaling  (egnn.py:183-188) ----
-  for (int idx = tid; idx < nvalid * D * (1 + NT); idx += kThreads) {
+  for (int idx = tid; idx < nvalid * D * (1 + NT); idx += kNT) {
     const int which = idx / (nvalid * D), nd = idx - which * nvalid * D, n = nd / D, d = nd - n * D;
     const int m = n / N;
     const int row = which * RP + n;
