@@ -81,7 +81,7 @@ __device__ inline float clip_end(float tn, float tau1) { return tn > tau1 - 1e-6
 template <int NF, int NT, int L, int D>
 __device__ __forceinline__ void joint_field(const Net& net, const Lds& s, const SolverLds& st, const SolveP& sp,
                                             float* kx_out, float* kl_out) {
-  constexpr int kThreads = Geo<NT>::NTHR;
+  constexpr int kThreads = Geo<NF, NT>::NTHR;
   const int tid = threadIdx.x, MPW = net.MPW, ND = net.ND;
   // NT == 0: one primal eval; Hutchinson: one JVP along eps; exact: ND JVPs along e_k (trace of J)
   const int nrep = (NT == 0 || sp.div == ECNF_DIV_HUTCHINSON) ? 1 : ND;
@@ -126,12 +126,12 @@ enum Phase { kEuler = 0, kInit0 = 1, kInit1 = 2, kFsal = 3, kStage = 4 };
 
 // The whole solve as a phase machine around ONE field evaluation per loop trip.
 template <int NF, int NT, int L, int D>
-__global__ __launch_bounds__(Geo<NT>::NTHR) void integrate_kernel(Net net, SolveP sp, const float* __restrict__ y0,
+__global__ __launch_bounds__((Geo<NF, NT>::NTHR)) void integrate_kernel(Net net, SolveP sp, const float* __restrict__ y0,
                                                                   const int32_t* __restrict__ feat,
                                                                   const float* __restrict__ eps, float* y1,
                                                                   float* dlogp, int32_t* nfe_out,
                                                                   int32_t* status_out, int B) {
-  constexpr int kThreads = Geo<NT>::NTHR;
+  constexpr int kThreads = Geo<NF, NT>::NTHR;
   extern __shared__ float smem[];
   const int tid = threadIdx.x, MPW = net.MPW, ND = net.ND, N = net.N;
   const Lds s = carve_lds<NT>(net, smem);
@@ -363,12 +363,12 @@ __global__ __launch_bounds__(Geo<NT>::NTHR) void integrate_kernel(Net net, Solve
 
 // one evaluation (and n_tangents JVPs) per molecule
 template <int NF, int NT, int L, int D>
-__global__ __launch_bounds__(Geo<NT>::NTHR) void vf_kernel(Net net, const float* __restrict__ x,
+__global__ __launch_bounds__((Geo<NF, NT>::NTHR)) void vf_kernel(Net net, const float* __restrict__ x,
                                                            const float* __restrict__ t,
                                                            const int32_t* __restrict__ feat,
                                                            const float* __restrict__ tan_in, int ntan, float* v,
                                                            float* tan_out, int B) {
-  constexpr int kThreads = Geo<NT>::NTHR;
+  constexpr int kThreads = Geo<NF, NT>::NTHR;
   extern __shared__ float smem[];
   const int tid = threadIdx.x, MPW = net.MPW, ND = net.ND, N = net.N;
   const Lds s = carve_lds<NT>(net, smem);
@@ -507,6 +507,48 @@ struct Packer {
   }
 };
 
+// bf16 round-to-nearest-even of a finite float, and back
+static inline uint16_t bf16_rne(float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+static inline float bf16_float(uint16_t b) {
+  const uint32_t u = (uint32_t)b << 16;
+  float f;
+  std::memcpy(&f, &u, 4);
+  return f;
+}
+
+// split-bf16 fragments of one [M][M] chain layer (chain_split.hpp): group g = (jb * NF + fb) * 2 + u, piece p,
+// lane l = (c, h), bf16 element j = W[32 fb + f(8u + j, h)][32 jb + c], f(r, h) = (r & 3) + 8 (r >> 2) + 4 h,
+// w = piece0 + piece1 + piece2 by successive RNE
+static void pack_split_layer(const float* W, int M, uint32_t* dst) {
+  const int NF = M / 32;
+  for (int jb = 0; jb < NF; ++jb)
+    for (int fb = 0; fb < NF; ++fb)
+      for (int u = 0; u < 2; ++u) {
+        const int g = (jb * NF + fb) * 2 + u;
+        for (int l = 0; l < 64; ++l)
+          for (int j = 0; j < 8; ++j) {
+            const int r = 8 * u + j, h = l >> 5;
+            const int in = 32 * fb + (r & 3) + 8 * (r >> 2) + 4 * h, out = 32 * jb + (l & 31);
+            const float w = W[(size_t)in * M + out];
+            uint16_t piece[3];
+            piece[0] = bf16_rne(w);
+            const float r1 = w - bf16_float(piece[0]);
+            piece[1] = bf16_rne(r1);
+            const float r2 = r1 - bf16_float(piece[1]);
+            piece[2] = bf16_rne(r2);
+            for (int p = 0; p < 3; ++p) {
+              uint32_t& word = dst[(((size_t)g * 3 + p) * 64 + l) * 4 + (j >> 1)];
+              word = (j & 1) ? ((word & 0x0000ffffu) | ((uint32_t)piece[p] << 16)) : ((word & 0xffff0000u) | piece[p]);
+            }
+          }
+      }
+}
+
 struct HostBlock {
   const float *xb, *xk, *gb, *gk;
   const float *eb[4], *ek[4];
@@ -557,7 +599,7 @@ hipError_t launch_integrate(const ecnf_handle* h, const SolveP& sp, const float*
   hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds[NT]);
   if (e != hipSuccess) return e;
   const int grid = (B + h->net[NT].MPW - 1) / h->net[NT].MPW;
-  hipLaunchKernelGGL(k, dim3(grid), dim3(Geo<NT>::NTHR), h->lds[NT], stream, h->net[NT], sp, y0, feat, eps, y1, dlogp,
+  hipLaunchKernelGGL(k, dim3(grid), dim3(Geo<NF, NT>::NTHR), h->lds[NT], stream, h->net[NT], sp, y0, feat, eps, y1, dlogp,
                      nfe, status, B);
   return hipGetLastError();
 }
@@ -569,7 +611,7 @@ hipError_t launch_vf(const ecnf_handle* h, const float* x, const float* t, const
   hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds[NT]);
   if (e != hipSuccess) return e;
   const int grid = (B + h->net[NT].MPW - 1) / h->net[NT].MPW;
-  hipLaunchKernelGGL(k, dim3(grid), dim3(Geo<NT>::NTHR), h->lds[NT], stream, h->net[NT], x, t, feat, tan_in, ntan, v,
+  hipLaunchKernelGGL(k, dim3(grid), dim3(Geo<NF, NT>::NTHR), h->lds[NT], stream, h->net[NT], x, t, feat, tan_in, ntan, v,
                      tan_out, B);
   return hipGetLastError();
 }
@@ -709,7 +751,7 @@ int ecnf_create(const ecnf_cfg* cfg, const float* params, size_t n_floats, int d
 
   // ---- repack ----
   Packer pk;
-  struct Off { size_t Wn, bn, Wp, bp, wd, We, be, wx, wg, Wh[kMaxPhiH], bh[kMaxPhiH]; float bx, bg; };
+  struct Off { size_t Wn, bn, Wp, bp, wd, We, Ws, be, wx, wg, Wh[kMaxPhiH], bh[kMaxPhiH]; float bx, bg; };
   std::vector<Off> off(K);
   for (int k = 0; k < K; ++k) {
     const HostBlock& b = hb[k];
@@ -745,6 +787,12 @@ int ecnf_create(const ecnf_cfg* cfg, const float* params, size_t n_floats, int d
       std::memcpy(be.data() + (size_t)cl * M, bb, M * sizeof(float));
     }
     o.We = pk.put(we.data(), we.size());
+    // the same chain as split-bf16 fragments: [layer][2 NF^2 groups][3 pieces][64 lanes][4 u32]
+    const size_t split_layer = (size_t)2 * NF * NF * 3 * 64 * 4;
+    std::vector<uint32_t> ws((size_t)nchain * split_layer, 0u);
+    for (int cl = 0; cl < nchain; ++cl)
+      pack_split_layer(cl < L - 1 ? b.ek[cl + 1] : b.tk[cl - (L - 1)], M, ws.data() + cl * split_layer);
+    o.Ws = pk.put(reinterpret_cast<const float*>(ws.data()), ws.size());
     o.be = pk.put(be.data(), be.size());
     o.wx = pk.put(b.xk, M);
     o.wg = pk.put(b.gk, M);
@@ -789,7 +837,7 @@ int ecnf_create(const ecnf_cfg* cfg, const float* params, size_t n_floats, int d
       BlockW& w = n.blk[k];
       const Off& o = off[k];
       w.Wn = dbuf + o.Wn; w.bn = dbuf + o.bn; w.Wp = dbuf + o.Wp; w.bp = dbuf + o.bp; w.wd = dbuf + o.wd;
-      w.We = dbuf + o.We; w.be = dbuf + o.be; w.wx = dbuf + o.wx; w.wg = dbuf + o.wg; w.bx = o.bx; w.bg = o.bg;
+      w.We = dbuf + o.We; w.Ws = reinterpret_cast<const unsigned*>(dbuf + o.Ws); w.be = dbuf + o.be; w.wx = dbuf + o.wx; w.wg = dbuf + o.wg; w.bx = o.bx; w.bg = o.bg;
       for (int l = 0; l <= L; ++l) { w.Wh[l] = dbuf + o.Wh[l]; w.bh[l] = dbuf + o.bh[l]; }
     }
     int mpw = 0, rp = 0;

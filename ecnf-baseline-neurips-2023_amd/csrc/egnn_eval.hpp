@@ -4,7 +4,7 @@
 // and EGCL.__call__ (ecnf/nets/egnn.py:49-114) of the reference, with forward-mode tangents (NT = 1) for the
 // divergence terms of ecnf/cnf/sample_and_log_prob.py:57-78.
 //
-// Layout (per workgroup = Geo<NT>::NW waves, MPW molecules):
+// Layout (per workgroup = Geo<NF, NT>::NW waves, MPW molecules):
 //   * node rows: molecule m, atom i -> row n = m*N + i, padded to RP = 32*ceil(MPW*N/32); tangent row of n is
 //     RP + n.  All node state lives in LDS as [row][feature] with odd leading dimensions (conflict-free
 //     column reads by 32 lanes).
@@ -31,13 +31,20 @@
 namespace ecnf {
 
 constexpr int kSimds = 4;   // SIMDs per CU
-// Waves per workgroup: the primal kernels run 8 waves = 2 per SIMD (<= 256 registers each), so one wave's VALU
-// work (SiLU, scans) overlaps the other wave's fp32 MFMA stream (measured: a co-resident VALU wave leaves the
-// MFMA wave at 64 cycles/MFMA, while VALU issued between a wave's OWN MFMAs adds ~5-11 cycles each).  The tangent
-// kernels carry twice the activations and keep 4 waves (1 per SIMD).
-template <int NT>
+// Edge-chain arithmetic: the primal kernels with M <= 128 run the chain on the bf16 matrix cores with
+// fp32-accurate operand splitting (chain_split.hpp); -DECNF_FP32_CHAIN builds the fp32-MFMA chain instead.
+#ifdef ECNF_FP32_CHAIN
+constexpr bool kSplitChain = false;
+#else
+constexpr bool kSplitChain = true;
+#endif
+// Waves per workgroup.  Split chain: 4 waves (one per SIMD, 512 registers: two activation buffers + the
+// accumulators of a tile).  fp32-MFMA chain, primal, M <= 128: 8 waves (2 per SIMD, <= 256 registers).
+// Tangent kernels and M = 256 carry twice the registers per tile: 4 waves.
+template <int NF, int NT>
 struct Geo {
-  static constexpr int NW = NT ? 4 : 8;
+  static constexpr bool kSplit = kSplitChain && NT == 0 && NF <= 4;
+  static constexpr int NW = (!kSplit && NT == 0 && NF <= 4) ? 8 : 4;
   static constexpr int NTHR = 64 * NW;
 };
 constexpr int kMaxBlocks = 10;
@@ -71,6 +78,7 @@ struct BlockW {
   const float* Wp;  const float* bp;    // [H][2M] = [W_send | W_recv] of phi_e.0, bias [2M] = [0 | b]
   const float* wd;                      // [M]  phi_e.0 kernel row 2H (the |r|^2 feature)
   const float* We;  const float* be;    // packed chain weights: phi_e.1..L-1 then phi_x.0..L-1, biases [(2L-1)][M]
+  const unsigned* Ws;                   // the same chain as split-bf16 fragments (chain_split.hpp)
   const float* wx;  const float* wg;    // [M] phi_x output Dense(1) kernel, [M] gate Dense(1) kernel
   float bx, bg;                         // their biases
   const float* Wh[kMaxPhiH]; const float* bh[kMaxPhiH];  // phi_h layers, row-major [in][out]
@@ -206,12 +214,13 @@ __device__ __forceinline__ void silu_dual(float p, float dp, float& y, float& dy
 
 // Returns `p` as a wave-uniform (SGPR) value the optimiser cannot see through: keeps per-tile weight loads inside
 // the tile loop (no LICM of a layer's weights into registers) and their addresses scalar.
-__device__ __forceinline__ const float* launder_uniform(const float* p) {
+template <typename T>
+__device__ __forceinline__ const T* launder_uniform(const T* p) {
   const uint64_t v = reinterpret_cast<uint64_t>(p);
   uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
   uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
   asm volatile("" : "+s"(lo), "+s"(hi));
-  return reinterpret_cast<const float*>(((uint64_t)hi << 32) | lo);
+  return reinterpret_cast<const T*>(((uint64_t)hi << 32) | lo);
 }
 
 __device__ __forceinline__ f32x4 ldg4(const float* p, int idx4) { return gptr4(p)[idx4]; }
@@ -363,21 +372,57 @@ __device__ __forceinline__ void node_gemm(const float* X1, int ldx1, int K1, con
 // The A fragments of one (output block jb, input block fb) group are 4 dwordx4 per lane (16 MFMAs); groups are
 // software-pipelined PF groups ahead so the L2 latency hides behind MFMAs (counted vmcnt, no vmcnt(0) stalls).
 // ---------------------------------------------------------------------------------------------------
-#ifndef ECNF_EXP_PF
-#define ECNF_EXP_PF 1
-#endif
 // One software pipeline over NL consecutive chain layers (phi_e 2..L, or phi_x 1..L), IN PLACE:
-// X <- silu(X W_l + b_l) for l = 0..NL-1.  Per layer the NF output blocks accumulate side by side (fb-major
-// group order: consecutive MFMAs hit different accumulators) and the SiLU of all blocks overwrites the input
-// once its last MFMA has issued, so a wave holds 16 NF activation + 16 NF accumulator registers (<= 256 total
-// at NF = 4: two waves per SIMD).  The weight stream is contiguous across layers; the PF-group prefetch runs
-// straight over layer boundaries and is pinned by a sched_barrier.
+// X <- silu(X W_l + b_l) for l = 0..NL-1, one 32-edge tile in registers.
+//
+// Group (l, g = fb * NF + jb) is 16 MFMAs that accumulate input block fb of X into output block jb; the NF output
+// blocks of a layer accumulate side by side, so a wave holds 16 NF activation + 16 NF accumulator registers.
+// The SiLU epilogue is NOT a burst at the layer end: an fp32 32x32x2 MFMA keeps the SIMD busy for 64 cycles but
+// holds its vector issue for only a few of them, so independent VALU placed between the wave's own MFMAs is
+// almost free (MI355X_MICROARCH.md, "vector-instruction ISSUE cost").  Output block j < NF-1 is final after group
+// (NF-1, j) and is activated (X[j] <- silu(acc[j] + b), in place: X[j] was last read by group (j, *)) one
+// element per MFMA slot during the next group; block NF-1 is activated during the first NF-1 groups of the next
+// layer, before group (0, NF-1) re-zeroes its accumulator and long before group (NF-1, *) reads it.  Only the
+// last layer's block NF-1 is left for a short tail.  sched_barriers pin this order and the weight prefetch
+// (PF groups ahead, contiguous across layers).
+#ifndef ECNF_EXP_PF
+#define ECNF_EXP_PF 2
+#endif
+template <int NF>
+struct ChainPlan {
+  // SiLU work of group g (0..NF*NF-1) of a layer l: {block, layer offset (0 = this layer, -1 = previous), first
+  // element, end element}; block -1 = none
+  struct Task { int j, dl, e0, e1; };
+  static constexpr Task task(int g, bool has_prev) {
+    if (g >= (NF - 1) * NF + 1) return Task{g - (NF - 1) * NF - 1, 0, 0, 16};
+    if (has_prev && g <= NF - 2) return Task{NF - 1, -1, (16 * g) / (NF - 1), (16 * (g + 1)) / (NF - 1)};
+    return Task{-1, 0, 0, 0};
+  }
+  // MFMA slot (1..15) after which element k of n is activated
+  static constexpr int slot(int k, int n) { return 1 + (k * 15) / (n > 0 ? n : 1); }
+};
+
+template <int NT>
+__device__ __forceinline__ void chain_act(f32x16& x, f32x16& xt, const f32x16& a, const f32x16& at, int r, float b) {
+  float y, yT = 0.f;
+#ifdef ECNF_EXP_NO_SILU
+  y = a[r] + b;
+  yT = NT ? at[r] : 0.f;
+#else
+  silu_dual<NT>(a[r] + b, NT ? at[r] : 0.f, y, yT);
+#endif
+  x[r] = y;
+  if constexpr (NT) xt[r] = yT;
+}
+
 template <int NF, int NT, int NL>
 __device__ __forceinline__ void chain_segment(f32x16 (&X)[NF], f32x16 (&XT)[NF], const float* __restrict__ Wpk,
                                               const float* __restrict__ bias /* LDS, [NL][M] */, int lane) {
   constexpr int GL = NF * NF;             // groups per layer, g = fb * NF + jb
   constexpr int G = NL * GL;
+  constexpr int M = NF * 32;
   constexpr int PF = ECNF_EXP_PF;         // groups in flight ahead of the MFMAs
+  using Plan = ChainPlan<NF>;
   const int kk = lane >> 5;
   const gf32x4_p wp = gptr4(Wpk) + lane;
   // group (l, jb, fb) sits at wp[((l * NF * NF + jb * NF + fb) * 4 + q) * 64]
@@ -391,57 +436,56 @@ __device__ __forceinline__ void chain_segment(f32x16 (&X)[NF], f32x16 (&XT)[NF],
 #pragma unroll
     for (int q = 0; q < 4; ++q) wbuf[gg][q] = wp[(gidx(gg) + q) * 64];
   f32x16 acc[NF], accT[NF];
+  f32x4 bb[4];                            // bias of the block being activated
   static_for<G>([&](auto GGc) {
     constexpr int gg = decltype(GGc)::value;
     constexpr int l = gg / GL, g = gg % GL, fb = g / NF, jb = g % NF;
+    constexpr typename Plan::Task tk = Plan::task(g, l > 0);
     if constexpr (gg + PF < G) {
+#ifndef ECNF_EXP_NO_WLOAD
 #pragma unroll
       for (int q = 0; q < 4; ++q) wbuf[(gg + PF) % (PF + 1)][q] = wp[(gidx(gg + PF) + q) * 64];
+#endif
     }
-#ifndef ECNF_EXP_NO_SCHED_BARRIER
+    if constexpr (tk.j >= 0 && tk.e0 == 0) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        bb[q] = *reinterpret_cast<const f32x4*>(bias + (l + tk.dl) * M + tk.j * 32 + 8 * q + 4 * kk);
+    }
     __builtin_amdgcn_sched_barrier(0);
-#endif
-    if constexpr (fb == 0) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        acc[jb][r] = 0.f;
-        if constexpr (NT) accT[jb][r] = 0.f;
+    static_for<16>([&](auto Ic) {
+      constexpr int i = decltype(Ic)::value, q = i >> 2, e = i & 3;
+      const float w = wbuf[gg % (PF + 1)][q][e];
+      if constexpr (fb == 0 && i == 0) {
+        const f32x16 z = {};
+        acc[jb] = mfma32(w, X[fb][i], z);
+        if constexpr (NT) accT[jb] = mfma32(w, XT[fb][i], z);
+      } else {
+        acc[jb] = mfma32(w, X[fb][i], acc[jb]);
+        if constexpr (NT) accT[jb] = mfma32(w, XT[fb][i], accT[jb]);
       }
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const f32x4 w = wbuf[gg % (PF + 1)][q];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        acc[jb] = mfma32(w[e], X[fb][4 * q + e], acc[jb]);
-        if constexpr (NT) accT[jb] = mfma32(w[e], XT[fb][4 * q + e], accT[jb]);
-      }
-    }
-    if constexpr (g == GL - 1) {
-      // layer complete: X <- silu(acc + b)  (Dense: x W, then + b; mlp.py:14)
-#pragma unroll
-      for (int j = 0; j < NF; ++j) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const f32x4 b4 = *reinterpret_cast<const f32x4*>(bias + l * (NF * 32) + j * 32 + 8 * q + 4 * kk);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int r = 4 * q + e;
-            float y, yT = 0.f;
-#ifdef ECNF_EXP_NO_SILU
-            y = acc[j][r] + b4[e];
-            yT = NT ? accT[j][r] : 0.f;
-#else
-            silu_dual<NT>(acc[j][r] + b4[e], NT ? accT[j][r] : 0.f, y, yT);
-#endif
-            X[j][r] = y;
-            if constexpr (NT) XT[j][r] = yT;
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (tk.j >= 0) {
+        constexpr int n = tk.e1 - tk.e0;
+        static_for<16>([&](auto Kc) {
+          constexpr int k = decltype(Kc)::value;
+          if constexpr (k < n && Plan::slot(k, n) == i) {
+            constexpr int r = tk.e0 + k;
+            chain_act<NT>(X[tk.j], XT[tk.j], acc[tk.j], accT[tk.j], r, bb[r >> 2][r & 3]);
           }
-        }
+        });
+        __builtin_amdgcn_sched_barrier(0);
       }
-    }
+    });
   });
+  // tail: the last layer's block NF-1
+#pragma unroll
+  for (int q = 0; q < 4; ++q) bb[q] = *reinterpret_cast<const f32x4*>(bias + (NL - 1) * M + (NF - 1) * 32 + 8 * q + 4 * kk);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) chain_act<NT>(X[NF - 1], XT[NF - 1], acc[NF - 1], accT[NF - 1], r, bb[r >> 2][r & 3]);
 }
+
+#include "chain_split.hpp"
 
 // Segmented (by receiver row) inclusive PREFIX sum over the 32 edge lanes of each half-wave, in DPP:
 // row_shr:1,2,4,8 inside each 16-lane row, then row_bcast:15 carries lane 15's running sum into lanes 16..31
@@ -533,10 +577,11 @@ __device__ __forceinline__ void edge_shift(const Net& net, const BlockW& bw, con
 }
 
 // gate, message aggregation, phi_x torso + output, shifts (egnn.py:81-104); `m` holds the messages
-template <int NF, int NT, int L, int D>
+template <int NF, int NT, int L, int D, typename PhiX>
 __device__ __forceinline__ void edge_tail(const Net& net, const BlockW& bw, const Lds& s, f32x16 (&X)[NF],
                                           f32x16 (&XT)[NF], bool valid, int rr, const float (&r)[D],
-                                          const float (&dr)[D], float length, float dlength, int lane) {
+                                          const float (&dr)[D], float length, float dlength, int lane,
+                                          PhiX&& phi_x) {
   f32x16(&m)[NF] = X;
   f32x16(&mT)[NF] = XT;
   const int kk = lane >> 5, li = lane & 31;
@@ -568,7 +613,9 @@ __device__ __forceinline__ void edge_tail(const Net& net, const BlockW& bw, cons
     float v[16];
 #pragma unroll
     for (int r16 = 0; r16 < 16; ++r16) v[r16] = m[fb][r16] * g;
+#ifndef ECNF_EXP_NO_AGG
     sc.sum_many<16>(v);
+#endif
     if (writer) {
 #pragma unroll
       for (int r16 = 0; r16 < 16; ++r16) lds_add(&s.macc[rr * s.ld_m + fb * 32 + acc_row(r16, kk)], v[r16]);
@@ -586,17 +633,35 @@ __device__ __forceinline__ void edge_tail(const Net& net, const BlockW& bw, cons
   }
 
   // phi_x torso (egnn.py:82) then its Dense(1) and the shifts
-  const float* We = bw.We + (L - 1) * NF * NF * 1024;
-  const float* be = s.vecs + (L - 1) * NF * 32;
-  We = launder_uniform(We);
-  chain_segment<NF, NT, L>(X, XT, We, be, lane);
+  phi_x(X, XT);
+#ifndef ECNF_EXP_NO_SHIFT
   edge_shift<NF, NT, L, D>(net, bw, s, X, XT, writer, sc, rr, r, dr, length, dlength, lane);
+#endif
 }
 
 // one 32-edge tile through phi_e / gate / phi_x  (egnn.py:72-95)
 template <int NF, int NT, int L, int D>
 __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, const Lds& s, int tile, int lane) {
   const int kk = lane >> 5, li = lane & 31;
+#ifdef ECNF_EXP_CHAIN_ONLY
+  {  // timing experiment: the two chain segments alone, on synthetic activations, one LDS add as the sink
+    f32x16 X[NF], XT[NF];
+#pragma unroll
+    for (int fb = 0; fb < NF; ++fb)
+#pragma unroll
+      for (int r16 = 0; r16 < 16; ++r16) X[fb][r16] = 0.01f * (fb * 16 + r16) + 1e-3f * lane + 1e-4f * tile;
+    chain_segment<NF, NT, L - 1>(X, XT, launder_uniform(bw.We), s.vecs, lane);
+    chain_segment<NF, NT, L>(X, XT, launder_uniform(bw.We + (L - 1) * NF * NF * 1024), s.vecs + (L - 1) * NF * 32,
+                             lane);
+    float acc = 0.f;
+#pragma unroll
+    for (int fb = 0; fb < NF; ++fb)
+#pragma unroll
+      for (int r16 = 0; r16 < 16; ++r16) acc += X[fb][r16];
+    lds_add(&s.dxacc[li], acc);
+    return;
+  }
+#endif
   const int N = net.N, E = net.E, nn1 = N - 1, RP = net.RP, M = NF * 32;
   // each molecule owns EP = 32*ceil(E/32) edge slots, so its tiles (and every rounding inside them) do not
   // depend on which slot of the workgroup, i.e. which batch position, it occupies
@@ -608,7 +673,8 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
   const int jj = el - i * nn1;
   int sd = i + 1 + jj;
   if (sd >= N) sd -= N;
-  const int rr = mol * N + i, rs = mol * N + sd;   // receiver / sender rows (graph.py:10-13)
+  const int mrow = valid ? mol : 0;
+  const int rr = mrow * N + i, rs = mrow * N + sd;   // receiver / sender rows (graph.py:10-13)
 #ifdef ECNF_STAMPS
   unsigned long long t_sub = __builtin_amdgcn_s_memtime();
 #endif
@@ -639,6 +705,47 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
     for (int d = 0; d < D; ++d) dr[d] = 0.f;
   }
 
+  if constexpr (Geo<NF, NT>::kSplit) {
+    // phi_e layer 1 from the per-node halves: pre = P_s[s] + P_r[r] + |r|^2 w_d  (egnn.py:76,79), SiLU, split
+    SplitX<NF> XA, XB;
+    f32x16 acc[NF];
+    const float* Ps = s.P + rs * s.ld_P;
+    const float* Pr = s.P + rr * s.ld_P + M;
+    static_for<NF>([&](auto Fc) {
+      constexpr int fb = decltype(Fc)::value;
+      static_for<4>([&](auto Qc) {
+        constexpr int q = decltype(Qc)::value;
+        const f32x4 w = *reinterpret_cast<const f32x4*>(s.vecs + (2 * L - 1) * (NF * 32) + fb * 32 + 8 * q + 4 * kk);
+        static_for<2>([&](auto Hc) {
+          constexpr int e = 2 * decltype(Hc)::value;
+          const int row = fb * 32 + 8 * q + 4 * kk + e;
+          const float p0 = Ps[row] + Pr[row] + len2 * w[e];
+          const float p1 = Ps[row + 1] + Pr[row + 1] + len2 * w[e + 1];
+          put_pair<NF, fb, 4 * q + e>(XA, p0 * sigmoidf_(p0), p1 * sigmoidf_(p1));
+        });
+      });
+    });
+    STAMP_LANE0(s, kStEdgeLayer1, t_sub);
+    // phi_e layers 2..L
+    const unsigned* Ws = launder_uniform(bw.Ws);
+    chain_split<NF, L - 1>(XA, XB, acc, Ws, s.vecs, lane);
+    STAMP_LANE0(s, kStEdgeChainE, t_sub);
+    edge_tail<NF, NT, L, D>(net, bw, s, acc, acc, valid, rr, r, dr, length, dlength, lane,
+                            [&](f32x16 (&m)[NF], f32x16 (&)[NF]) {
+                              // phi_x layers 1..L on the (ungated) messages
+                              static_for<NF>([&](auto Fc) {
+                                constexpr int fb = decltype(Fc)::value;
+                                static_for<8>([&](auto Ic) {
+                                  constexpr int i = decltype(Ic)::value;
+                                  put_pair<NF, fb, 2 * i>(XA, m[fb][2 * i], m[fb][2 * i + 1]);
+                                });
+                              });
+                              const unsigned* Wx = launder_uniform(bw.Ws + (size_t)(L - 1) * SplitPlan<NF>::GL * 768);
+                              chain_split<NF, L>(XA, XB, m, Wx, s.vecs + (L - 1) * NF * 32, lane);
+                            });
+    STAMP_LANE0(s, kStEdgeTail, t_sub);
+    return;
+  }
   // phi_e layer 1 from the per-node halves: pre = P_s[s] + P_r[r] + |r|^2 w_d  (egnn.py:76,79)
   f32x16 X[NF], XT[NF];
   const float* Ps = s.P + rs * s.ld_P;
@@ -653,7 +760,11 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
 #pragma unroll
       for (int e4 = 0; e4 < 4; ++e4) {
         const int row = fb * 32 + 8 * q + 4 * kk + e4;
+#ifdef ECNF_EXP_NO_L1GATHER
+        const float p = 0.01f * row + len2 * w[e4];
+#else
         const float p = Ps[row] + Pr[row] + len2 * w[e4];
+#endif
         float y, yT = 0.f;
         if constexpr (NT) {
           const float pT = PsT[row] + PrT[row] + dlen2 * w[e4];
@@ -671,7 +782,11 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
   const float* We = launder_uniform(bw.We);
   chain_segment<NF, NT, L - 1>(X, XT, We, s.vecs, lane);
   STAMP_LANE0(s, kStEdgeChainE, t_sub);
-  edge_tail<NF, NT, L, D>(net, bw, s, X, XT, valid, rr, r, dr, length, dlength, lane);
+  edge_tail<NF, NT, L, D>(net, bw, s, X, XT, valid, rr, r, dr, length, dlength, lane,
+                          [&](f32x16 (&Y)[NF], f32x16 (&YT)[NF]) {
+                            const float* Wx = launder_uniform(bw.We + (L - 1) * NF * NF * 1024);
+                            chain_segment<NF, NT, L>(Y, YT, Wx, s.vecs + (L - 1) * NF * 32, lane);
+                          });
   STAMP_LANE0(s, kStEdgeTail, t_sub);
 }
 
@@ -682,7 +797,7 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
 template <int NF, int NT, int L, int D>
 __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const float* x_in, const float* t_in, const float* tan_in,
                           float* v_out, float* tan_out) {
-  constexpr int kNW = Geo<NT>::NW, kNT = Geo<NT>::NTHR;
+  constexpr int kNW = Geo<NF, NT>::NW, kNT = Geo<NF, NT>::NTHR;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int N = net.N, H = net.H, T = net.T, M = NF * 32, RP = net.RP, MPW = net.MPW, ND = net.ND;
   const int nvalid = MPW * N;
@@ -749,7 +864,13 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
     STAMP(s, kStPGemm);
     // edges
     // tile t runs on wave t mod NW, i.e. SIMD t mod 4: every SIMD gets ceil/floor(ntiles / 4) tiles
-    for (int tile = wave; tile < ntiles; tile += kNW) edge_tile<NF, NT, L, D>(net, bw, s, tile, lane);
+#ifdef ECNF_EXP_BALANCED
+    // timing experiment: every wave runs the same number of tiles (padding tiles are invalid)
+    const int ntiles_run = ((ntiles + kNW - 1) / kNW) * kNW;
+#else
+    const int ntiles_run = ntiles;
+#endif
+    for (int tile = wave; tile < ntiles_run; tile += kNW) edge_tile<NF, NT, L, D>(net, bw, s, tile, lane);
     __syncthreads();
     STAMP(s, kStEdge);
     // node update: x += shift_i / (N-1) (egnn.py:95,113); m_i /= sqrt(N-1) (egnn.py:104)
