@@ -8,8 +8,10 @@ One "step" = one full sample of the batch: x0 (resident in HBM) -> 100 EGNN eval
 ecnf_integrate launch.  Multi-GPU: one process per GPU (torchrun), each rank samples its own 1024 molecules
 (weak scaling, no data-path collective); the timing is the max over ranks.
 
-Extra fields: "roofline" (dominant kernel = integrate_kernel, FP32-MFMA bound: algorithmic FLOPs per launch /
-average launch time from HIP events on the launch stream) and "cpu_baseline" (the oracle's numpy fp32 batched
+Extra fields: "roofline" (dominant kernel = integrate_kernel, MFMA bound: algorithmic fp32 FLOPs per launch /
+average launch time from HIP events on the launch stream, against the ceiling of the kernel's instruction mix —
+edge-chain FLOPs at the split-bf16 rate, the rest at the fp32 MFMA rate; see roofline_peak), "matmul" (which
+arithmetic each GEMM family runs) and "cpu_baseline" (the oracle's numpy fp32 batched
 restatement of the same Euler solve on a bounded sample, rank 0 at N = 1 only).
 """
 from __future__ import annotations
@@ -24,7 +26,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "ecnf-baseline-neurips-2023_amd"))
 sys.path.insert(0, ROOT)
 
-PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X dense FP32 matrix peak (MI355X_MICROARCH.md, chip-level parameters)
+PEAK_FP32_MFMA_TFLOPS = 157.3    # MI355X dense FP32 matrix peak (MI355X_MICROARCH.md, chip-level parameters)
+PEAK_BF16_MFMA_TFLOPS = 2516.6   # MI355X dense BF16 matrix peak: 256 CU x 4 SIMD x 1024 FLOP/clk x 2.4 GHz
+SPLIT_TERMS = 6                  # bf16 cross terms per fp32 product in the split chain (chain_split.hpp)
 
 
 def flops_per_eval(cfg) -> float:
@@ -35,6 +39,22 @@ def flops_per_eval(cfg) -> float:
     E = N * (N - 1)
     return K * (2 * N * (H + T) * H + 4 * N * H * M + 3 * E * M + 2 * E * (L - 1) * M * M + 2 * E * L * M * M
                 + 4 * E * M + 2 * N * ((M + H) * M + (L - 1) * M * M + M * H))
+
+
+def chain_flops_per_eval(cfg) -> float:
+    """The edge-MLP chain part of flops_per_eval: phi_e layers 2..L and phi_x layers 1..L on every edge."""
+    N, M, L, K = cfg.n_nodes, cfg.mlp_width, cfg.mlp_depth, cfg.n_blocks
+    E = N * (N - 1)
+    return K * (2 * E * (L - 1) * M * M + 2 * E * L * M * M)
+
+
+def roofline_peak(cfg, chain_mode: str) -> float:
+    """Ceiling (TFLOP/s of algorithmic fp32 FLOPs) for this kernel's instruction mix: the chain FLOPs at the
+    split-bf16 rate (dense bf16 peak / 6 terms) when the chain runs split, everything else at the fp32 MFMA peak;
+    peak = F / (F_chain / P_chain + F_rest / P_fp32)."""
+    F, Fc = flops_per_eval(cfg), chain_flops_per_eval(cfg)
+    p_chain = PEAK_BF16_MFMA_TFLOPS / SPLIT_TERMS if chain_mode == "split_bf16" else PEAK_FP32_MFMA_TFLOPS
+    return F / (Fc / p_chain + (F - Fc) / PEAK_FP32_MFMA_TFLOPS)
 
 
 def cpu_baseline(cfg_name: str, n_mol: int, nfe: int, threads: int):
@@ -129,6 +149,8 @@ def main():
     value = world * args.batch * args.steps / t_max
     F = flops_per_eval(cfg)
     achieved = F * nfe_seen * args.batch / (kernel_ms * 1e-3) / 1e12
+    chain_mode = h.chain_arithmetic()
+    peak = roofline_peak(cfg, chain_mode)
 
     traffic = None
     pmc = os.path.join(ROOT, "profiles", f"pmc_traffic_{args.config}_b{args.batch}.json")
@@ -161,10 +183,13 @@ def main():
             "config": {"workload": f"{args.config} sample, Euler NFE={nfe_seen}, batch {args.batch}/GPU",
                        "n_nodes": cfg.n_nodes, "batch_per_gpu": args.batch, "global_batch": world * args.batch,
                        "nfe": nfe_seen, "solver": "euler", "parallelism": f"dp{world}"},
-            "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved / PEAK_FP32_MFMA_TFLOPS, "traffic": traffic,
+            "matmul": {"edge_chain": chain_mode, "node_gemms": "fp32_mfma", "accumulate": "f32"},
+            "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
+                         "frac": achieved / peak, "traffic": traffic,
                          "kernel": "integrate_kernel", "kernel_ms": kernel_ms,
-                         "flop_per_launch": F * nfe_seen * args.batch},
+                         "flop_per_launch": F * nfe_seen * args.batch,
+                         "peak_basis": "chain FLOPs at dense bf16 peak / 6 split terms, other FLOPs at fp32 MFMA "
+                                       "peak" if chain_mode == "split_bf16" else "fp32 MFMA peak"},
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

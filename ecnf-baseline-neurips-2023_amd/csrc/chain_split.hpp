@@ -83,15 +83,27 @@ struct SplitPlan {
   static constexpr int slot(int i, int n) { return 1 + (i * 5) / (n > 0 ? n : 1); }
 };
 
-// element pair activation: y = silu(acc + b) (Dense then SiLU, mlp.py:14), either split into X or fp32 in place
+// element pair activation: y = silu(acc + b) (Dense then SiLU, mlp.py:14), either split into X or fp32 in place;
+// b2 = the biases of rows (R, R+1)
 template <int NF, int J, int R, bool SPLIT>
-__device__ __forceinline__ void act_pair(f32x16 (&acc)[NF], SplitX<NF>& X, const f32x4 (&bb)[4]) {
-  const float t0 = acc[J][R] + bb[R >> 2][R & 3];
-  const float t1 = acc[J][R + 1] + bb[(R + 1) >> 2][(R + 1) & 3];
+__device__ __forceinline__ void act_pair(f32x16 (&acc)[NF], SplitX<NF>& X, f32x2 b2) {
+#ifdef ECNF_SPLIT_CHEAP_ACT   // timing experiment: keep the data flow, drop the arithmetic
+  if constexpr (SPLIT) {
+    X.v[J][R >> 3][0][(R & 7) >> 1] = __builtin_bit_cast(unsigned, acc[J][R]);
+    X.v[J][R >> 3][1][(R & 7) >> 1] = __builtin_bit_cast(unsigned, acc[J][R + 1]);
+  }
+  return;
+#endif
+  const float t0 = acc[J][R] + b2[0];
+  const float t1 = acc[J][R + 1] + b2[1];
   const float y0 = t0 * sigmoidf_(t0);
   const float y1 = t1 * sigmoidf_(t1);
   if constexpr (SPLIT) {
+#ifdef ECNF_SPLIT_NO_SPLIT
+    X.v[J][R >> 3][0][(R & 7) >> 1] = __builtin_bit_cast(unsigned, y0) ^ __builtin_bit_cast(unsigned, y1);
+#else
     put_pair<NF, J, R>(X, y0, y1);
+#endif
   } else {
     acc[J][R] = y0;
     acc[J][R + 1] = y1;
@@ -107,44 +119,67 @@ __device__ __forceinline__ auto& pick(A& a, B& b) {
 #define ECNF_SPLIT_PF 3
 #endif
 
+__device__ __forceinline__ u32x4 wload(__amdgpu_buffer_rsrc_t rsrc, int voff, int soff) {
+  return __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, soff, 0);
+}
+
 // NL chained layers Y = silu(X W_l + b_l).  Input in XA (split form); on return acc holds the last layer's
 // activations in fp32 (accumulator layout).  XA / XB are both clobbered.
-// Weights: packed split-bf16 fragments [layer][group][piece][lane] (u32x4), biases: LDS [NL][M].
+// Weights: packed split-bf16 fragments [layer][group][piece][lane] (16 B), read as buffer loads with the group
+// offset in an SGPR; biases: LDS [NL][M], each activated pair's two (adjacent) rows read one group ahead.
+// Each group's MFMAs and activation VALU are emitted together and interleaved by sched_group_barrier: the
+// weight loads first, then MFMA / VALU alternately, so the VALU fills the MFMAs' free issue cycles.
 template <int NF, int NL>
 __device__ __forceinline__ void chain_split(SplitX<NF>& XA, SplitX<NF>& XB, f32x16 (&acc)[NF],
                                             const unsigned* __restrict__ Wpk, const float* __restrict__ bias,
                                             int lane) {
   using Plan = SplitPlan<NF>;
   constexpr int GB = Plan::GB, GL = Plan::GL, G = NL * GL, M = NF * 32, PF = ECNF_SPLIT_PF;
+  constexpr int kMaxPair = 8;
   const int kk = lane >> 5;
-  const gu32x4_p wp = (gu32x4_p)(Wpk) + lane;   // group gg, piece p: wp[(gg * 3 + p) * 64]
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned*>(Wpk), (short)0,
+                                                                         0x7fffffff, 0x00020000);
+  const int voff = lane * 16;
+  // task of global group gg (any layer), and the LDS bias address of its pair i
+  auto task_of = [](int gg2) constexpr { return Plan::task(gg2 % GL, gg2 / GL > 0); };
+  auto bias_row = [](int gg2, int i) constexpr {
+    const typename Plan::Task t = Plan::task(gg2 % GL, gg2 / GL > 0);
+    const int r = 2 * (t.p0 + i);
+    return (gg2 / GL + t.dl) * M + t.j * 32 + 8 * (r >> 2) + (r & 3);
+  };
   u32x4 wbuf[PF + 1][3];
 #pragma unroll
   for (int gg = 0; gg < PF && gg < G; ++gg)
 #pragma unroll
-    for (int p = 0; p < 3; ++p) wbuf[gg][p] = wp[(gg * 3 + p) * 64];
-  f32x4 bb[4];
+    for (int p = 0; p < 3; ++p) wbuf[gg][p] = wload(rsrc, voff, (gg * 3 + p) * 1024);
+  f32x2 bcur[kMaxPair], bnext[kMaxPair];
+  {
+    constexpr typename Plan::Task t0 = Plan::task(0, false);
+    if constexpr (t0.j >= 0)
+      static_for<t0.p1 - t0.p0>([&](auto Ic) {
+        bcur[Ic] = *reinterpret_cast<const f32x2*>(bias + bias_row(0, Ic) + 4 * kk);
+      });
+  }
   static_for<G>([&](auto GGc) {
     constexpr int gg = decltype(GGc)::value;
     constexpr int l = gg / GL, g = gg % GL, jb = g / GB, fb = (g % GB) >> 1, u = g & 1;
-    constexpr typename Plan::Task tk = Plan::task(g, l > 0);
+    constexpr typename Plan::Task tk = task_of(gg);
     constexpr int tl = l + tk.dl;                          // layer whose block is activated here
     constexpr bool split_out = tl < NL - 1;                // final layer stays fp32 in acc
+    constexpr int npair = tk.j >= 0 ? tk.p1 - tk.p0 : 0;
     auto& Xin = pick<l & 1>(XA, XB);
     auto& Xact = pick<(tl + 1) & 1>(XA, XB);               // the activated layer's output buffer
     if constexpr (gg + PF < G) {
 #pragma unroll
-      for (int p = 0; p < 3; ++p) wbuf[(gg + PF) % (PF + 1)][p] = wp[((gg + PF) * 3 + p) * 64];
+      for (int p = 0; p < 3; ++p) wbuf[(gg + PF) % (PF + 1)][p] = wload(rsrc, voff, ((gg + PF) * 3 + p) * 1024);
     }
-    if constexpr (tk.j >= 0 && tk.p0 == 0) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        bb[q] = *reinterpret_cast<const f32x4*>(bias + tl * M + tk.j * 32 + 8 * q + 4 * kk);
-    }
-    __builtin_amdgcn_sched_barrier(0);
+    // biases of the next group's pairs
+    constexpr int nnext = (gg + 1 < G && task_of(gg + 1).j >= 0) ? task_of(gg + 1).p1 - task_of(gg + 1).p0 : 0;
+    static_for<nnext>([&](auto Ic) {
+      bnext[Ic] = *reinterpret_cast<const f32x2*>(bias + bias_row(gg + 1, Ic) + 4 * kk);
+    });
     const u32x4* A = wbuf[gg % (PF + 1)];
     const u32x4* B = Xin.v[fb][u];
-    constexpr int npair = tk.j >= 0 ? tk.p1 - tk.p0 : 0;
     static_for<6>([&](auto Tc) {
       constexpr int t = decltype(Tc)::value;
       // cross terms, smallest first: (2,0) (1,1) (0,2) (1,0) (0,1) (0,0)  [weight piece, activation piece]
@@ -156,25 +191,32 @@ __device__ __forceinline__ void chain_split(SplitX<NF>& XA, SplitX<NF>& XB, f32x
       } else {
         acc[jb] = mfma_bf16(A[pa], B[pb], acc[jb]);
       }
-      __builtin_amdgcn_sched_barrier(0);
-      if constexpr (npair > 0) {
-        static_for<8>([&](auto Ic) {
-          constexpr int i = decltype(Ic)::value;
-          if constexpr (i < npair && Plan::slot(i, npair) == t) {
-            act_pair<NF, (tk.j < 0 ? 0 : tk.j), 2 * (tk.p0 + i), split_out>(acc, Xact, bb);
-          }
-        });
-        __builtin_amdgcn_sched_barrier(0);
-      }
     });
+#ifndef ECNF_SPLIT_NO_ACT
+    static_for<npair>([&](auto Ic) {
+      constexpr int i = decltype(Ic)::value;
+      act_pair<NF, (tk.j < 0 ? 0 : tk.j), 2 * (tk.p0 + i), split_out>(acc, Xact, bcur[i]);
+    });
+#endif
+    // schedule: weight loads, bias reads, then MFMA / VALU alternating
+    constexpr int nvalu = npair * (split_out ? 30 : 14);
+    constexpr int per = (nvalu + 5) / 6;
+#ifndef ECNF_SPLIT_NO_SGB
+    if constexpr (gg + PF < G) __builtin_amdgcn_sched_group_barrier(0x020, 3, 0);
+    if constexpr (nnext > 0) __builtin_amdgcn_sched_group_barrier(0x100, nnext, 0);
+    static_for<6>([&](auto) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      if constexpr (per > 0) __builtin_amdgcn_sched_group_barrier(0x002, per, 0);
+    });
+#endif
+    __builtin_amdgcn_sched_barrier(0);
+    static_for<nnext>([&](auto Ic) { bcur[Ic] = bnext[Ic]; });
   });
   // the final layer's last block
-#pragma unroll
-  for (int q = 0; q < 4; ++q)
-    bb[q] = *reinterpret_cast<const f32x4*>(bias + (NL - 1) * M + (NF - 1) * 32 + 8 * q + 4 * kk);
   static_for<8>([&](auto Ic) {
     constexpr int i = decltype(Ic)::value;
-    act_pair<NF, NF - 1, 2 * i, false>(acc, XA, bb);
+    const f32x2 b2 = *reinterpret_cast<const f32x2*>(bias + (NL - 1) * M + (NF - 1) * 32 + 8 * ((2 * i) >> 2) +
+                                                     ((2 * i) & 3) + 4 * kk);
+    act_pair<NF, NF - 1, 2 * i, false>(acc, XA, b2);
   });
 }
-

@@ -617,6 +617,10 @@ hipError_t launch_vf(const ecnf_handle* h, const float* x, const float* t, const
 }
 
 // compiled shapes: (M, L, D) with tangent support where registers allow (M <= 128)
+#ifdef ECNF_DEV_LJ13_ONLY   // experiment builds (tools/build_variants.sh): the LJ13 shape only
+#define ECNF_SHAPES(X) X(128, 3, 3)
+#define ECNF_SHAPES_PRIMAL_ONLY(X)
+#else
 #define ECNF_SHAPES(X)  \
   X(128, 3, 3)          \
   X(128, 3, 2)          \
@@ -630,6 +634,7 @@ hipError_t launch_vf(const ecnf_handle* h, const float* x, const float* t, const
 #define ECNF_SHAPES_PRIMAL_ONLY(X) \
   X(256, 4, 3)                     \
   X(256, 3, 3)
+#endif
 
 bool shape_supported(const ecnf_cfg& c, int NT) {
   const int M = c.mlp_width, L = c.mlp_depth, D = c.dim;
@@ -873,6 +878,13 @@ int ecnf_destroy(ecnf_handle* h) {
 int ecnf_molecules_per_workgroup(ecnf_handle* h, int32_t with_tangent, int32_t* mpw) {
   if (!h || !mpw) return fail(ECNF_E_INVALID, "NULL argument");
   *mpw = h->net[with_tangent ? 1 : 0].MPW;
+  return ECNF_OK;
+}
+
+int ecnf_chain_arithmetic(ecnf_handle* h, int32_t with_tangent, int32_t* mode) {
+  if (!h || !mode) return fail(ECNF_E_INVALID, "NULL argument");
+  const bool split = kSplitChain && !with_tangent && h->cfg.mlp_width <= 128;   // Geo<NF, NT>::kSplit
+  *mode = split ? ECNF_CHAIN_SPLIT_BF16 : ECNF_CHAIN_FP32_MFMA;
   return ECNF_OK;
 }
 

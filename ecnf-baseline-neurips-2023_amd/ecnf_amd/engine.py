@@ -117,6 +117,12 @@ class EcnfHandle:
         _lib.check(self.lib.ecnf_molecules_per_workgroup(self._h, int(with_tangent), ctypes.byref(v)))
         return v.value
 
+    def chain_arithmetic(self, with_tangent: bool = False) -> str:
+        """'split_bf16' (fp32-accurate 3-piece bf16 split, chain_split.hpp) or 'fp32_mfma'."""
+        v = ctypes.c_int32()
+        _lib.check(self.lib.ecnf_chain_arithmetic(self._h, int(with_tangent), ctypes.byref(v)))
+        return "split_bf16" if v.value == _lib.CHAIN_SPLIT_BF16 else "fp32_mfma"
+
     # ---------------------------------------------------------------------------------- C-ABI calls
     def vector_field(self, x, t, feat) -> torch.Tensor:
         """cnf.apply(params, x[B, N*D], t[B], features[B, N]) (core.py:7-19)."""

@@ -119,6 +119,14 @@ int ecnf_base_log_prob(ecnf_handle* h, const float* y, float* log_p, int32_t bat
 /* Molecules processed by one workgroup for this handle (diagnostic; kernels pick it from the LDS budget). */
 int ecnf_molecules_per_workgroup(ecnf_handle* h, int32_t with_tangent, int32_t* mpw);
 
+/* Arithmetic of the edge-MLP chain GEMMs (the bulk of the FLOPs) in this handle's kernels (diagnostic):
+ *   ECNF_CHAIN_FP32_MFMA   v_mfma_f32_32x32x2_f32, fp32 operands
+ *   ECNF_CHAIN_SPLIT_BF16  fp32 operands split into three bf16 pieces (RNE), the six cross terms above 2^-25 of
+ *                          the product on v_mfma_f32_32x32x16_bf16, fp32 accumulation (fp32-accurate) */
+#define ECNF_CHAIN_FP32_MFMA 0
+#define ECNF_CHAIN_SPLIT_BF16 1
+int ecnf_chain_arithmetic(ecnf_handle* h, int32_t with_tangent, int32_t* mode);
+
 /* Thread-local description of the last error ("" when none). */
 const char* ecnf_last_error(void);
 
