@@ -69,13 +69,16 @@ template <int NF>
 struct SplitPlan {
   static constexpr int GB = 2 * NF;        // groups per output block
   static constexpr int GL = NF * GB;       // groups per layer
-  static constexpr int WIN = 2 * NF - 2;   // groups of the next layer available to the last block
+  // groups of the next layer available to the last block: its split (stage 2) runs one group after its SiLU
+  // (stage 1) and must land before group (jb 0, fb NF-1) reads it
+  static constexpr int WIN = 2 * NF - 3 > 0 ? 2 * NF - 3 : 1;
   // activation work of group g of a layer: {block, layer offset, first pair, end pair}; block -1 = none.
   // pairs are 0..7 (16 elements of a block)
   struct Task { int j, dl, p0, p1; };
   static constexpr Task task(int g, bool has_prev) {
     const int jb = g / GB, k = g % GB;
-    if (jb >= 1) return Task{jb - 1, 0, (8 * k) / GB, (8 * (k + 1)) / GB};
+    // block jb-1 during the first GB-1 groups of block jb (its stage 2 then lands inside this layer)
+    if (jb >= 1) return k < GB - 1 ? Task{jb - 1, 0, (8 * k) / (GB - 1), (8 * (k + 1)) / (GB - 1)} : Task{-1, 0, 0, 0};
     if (has_prev && k < WIN) return Task{NF - 1, -1, (8 * k) / WIN, (8 * (k + 1)) / WIN};
     return Task{-1, 0, 0, 0};
   }
@@ -108,6 +111,22 @@ __device__ __forceinline__ void act_pair(f32x16 (&acc)[NF], SplitX<NF>& X, f32x2
     acc[J][R] = y0;
     acc[J][R + 1] = y1;
   }
+}
+
+// the activation in two stages, one group apart (software pipelined for ILP):
+//   stage 1: y = silu(acc + b) -> y2 (kept fp32 in place in acc for the final layer)
+//   stage 2: split y2 into the three bf16 pieces of the next layer's input
+template <int NF, int J, int R, bool SPLIT>
+__device__ __forceinline__ f32x2 act_stage1(f32x16 (&acc)[NF], f32x2 b2) {
+  const float t0 = acc[J][R] + b2[0];
+  const float t1 = acc[J][R + 1] + b2[1];
+  const float y0 = t0 * sigmoidf_(t0);
+  const float y1 = t1 * sigmoidf_(t1);
+  if constexpr (!SPLIT) {
+    acc[J][R] = y0;
+    acc[J][R + 1] = y1;
+  }
+  return f32x2{y0, y1};
 }
 
 template <int I, typename A, typename B>
@@ -153,6 +172,7 @@ __device__ __forceinline__ void chain_split(SplitX<NF>& XA, SplitX<NF>& XB, f32x
 #pragma unroll
     for (int p = 0; p < 3; ++p) wbuf[gg][p] = wload(rsrc, voff, (gg * 3 + p) * 1024);
   f32x2 bcur[kMaxPair], bnext[kMaxPair];
+  f32x2 ybuf[2][kMaxPair];                                // stage-1 results, by group parity
   {
     constexpr typename Plan::Task t0 = Plan::task(0, false);
     if constexpr (t0.j >= 0)
@@ -168,7 +188,6 @@ __device__ __forceinline__ void chain_split(SplitX<NF>& XA, SplitX<NF>& XB, f32x
     constexpr bool split_out = tl < NL - 1;                // final layer stays fp32 in acc
     constexpr int npair = tk.j >= 0 ? tk.p1 - tk.p0 : 0;
     auto& Xin = pick<l & 1>(XA, XB);
-    auto& Xact = pick<(tl + 1) & 1>(XA, XB);               // the activated layer's output buffer
     if constexpr (gg + PF < G) {
 #pragma unroll
       for (int p = 0; p < 3; ++p) wbuf[(gg + PF) % (PF + 1)][p] = wload(rsrc, voff, ((gg + PF) * 3 + p) * 1024);
@@ -193,13 +212,26 @@ __device__ __forceinline__ void chain_split(SplitX<NF>& XA, SplitX<NF>& XB, f32x
       }
     });
 #ifndef ECNF_SPLIT_NO_ACT
+    // stage 2 of the previous group's pairs (split into that layer's output buffer)
+    if constexpr (gg > 0) {
+      constexpr typename Plan::Task tp = task_of(gg - 1);
+      constexpr int lp = (gg - 1) / GL + tp.dl;
+      if constexpr (tp.j >= 0 && lp < NL - 1) {
+        auto& Xp = pick<(lp + 1) & 1>(XA, XB);
+        static_for<tp.p1 - tp.p0>([&](auto Ic) {
+          constexpr int i = decltype(Ic)::value;
+          put_pair<NF, tp.j, 2 * (tp.p0 + i)>(Xp, ybuf[(gg - 1) & 1][i][0], ybuf[(gg - 1) & 1][i][1]);
+        });
+      }
+    }
+    // stage 1 of this group's pairs
     static_for<npair>([&](auto Ic) {
       constexpr int i = decltype(Ic)::value;
-      act_pair<NF, (tk.j < 0 ? 0 : tk.j), 2 * (tk.p0 + i), split_out>(acc, Xact, bcur[i]);
+      ybuf[gg & 1][i] = act_stage1<NF, (tk.j < 0 ? 0 : tk.j), 2 * (tk.p0 + i), split_out>(acc, bcur[i]);
     });
 #endif
     // schedule: weight loads, bias reads, then MFMA / VALU alternating
-    constexpr int nvalu = npair * (split_out ? 30 : 14);
+    constexpr int nvalu = npair * 16 + 12 * ((gg > 0 && task_of(gg - 1).j >= 0) ? task_of(gg - 1).p1 - task_of(gg - 1).p0 : 0);
     constexpr int per = (nvalu + 5) / 6;
 #ifndef ECNF_SPLIT_NO_SGB
     if constexpr (gg + PF < G) __builtin_amdgcn_sched_group_barrier(0x020, 3, 0);
@@ -212,6 +244,17 @@ __device__ __forceinline__ void chain_split(SplitX<NF>& XA, SplitX<NF>& XB, f32x
     __builtin_amdgcn_sched_barrier(0);
     static_for<nnext>([&](auto Ic) { bcur[Ic] = bnext[Ic]; });
   });
+  {
+    constexpr typename Plan::Task tp = task_of(G - 1);
+    constexpr int lp = (G - 1) / GL + tp.dl;
+    if constexpr (tp.j >= 0 && lp < NL - 1) {
+      auto& Xp = pick<(lp + 1) & 1>(XA, XB);
+      static_for<tp.p1 - tp.p0>([&](auto Ic) {
+        constexpr int i = decltype(Ic)::value;
+        put_pair<NF, tp.j, 2 * (tp.p0 + i)>(Xp, ybuf[(G - 1) & 1][i][0], ybuf[(G - 1) & 1][i][1]);
+      });
+    }
+  }
   // the final layer's last block
   static_for<8>([&](auto Ic) {
     constexpr int i = decltype(Ic)::value;

@@ -521,6 +521,34 @@ static inline float bf16_float(uint16_t b) {
   return f;
 }
 
+// w = piece0 + piece1 + piece2 by successive RNE; stores bf16 element j of a lane's 8-element fragment
+static inline void put_split(uint32_t* frag_p0, size_t piece_stride, int j, float w) {
+  uint16_t piece[3];
+  piece[0] = bf16_rne(w);
+  const float r1 = w - bf16_float(piece[0]);
+  piece[1] = bf16_rne(r1);
+  const float r2 = r1 - bf16_float(piece[1]);
+  piece[2] = bf16_rne(r2);
+  for (int p = 0; p < 3; ++p) {
+    uint32_t& word = frag_p0[p * piece_stride + (j >> 1)];
+    word = (j & 1) ? ((word & 0x0000ffffu) | ((uint32_t)piece[p] << 16)) : ((word & 0xffff0000u) | piece[p]);
+  }
+}
+
+// split-bf16 fragments of a node GEMM W [K][NOUT] (row-major, node_task_split): [out block b][k-step s][piece]
+// [lane l][8 bf16], element j = W[16 s + 8 (l >> 5) + j][32 b + (l & 31)], zero for k >= K
+static void pack_split_node(const float* W, int K, int NOUT, uint32_t* dst) {
+  const int nks = (K + 15) / 16;
+  for (int b = 0; b < NOUT / 32; ++b)
+    for (int ks = 0; ks < nks; ++ks)
+      for (int l = 0; l < 64; ++l)
+        for (int j = 0; j < 8; ++j) {
+          const int k = 16 * ks + 8 * (l >> 5) + j;
+          const float w = k < K ? W[(size_t)k * NOUT + 32 * b + (l & 31)] : 0.f;
+          put_split(dst + (((size_t)b * nks + ks) * 3 * 64 + l) * 4, 64 * 4, j, w);
+        }
+}
+
 // split-bf16 fragments of one [M][M] chain layer (chain_split.hpp): group g = (jb * NF + fb) * 2 + u, piece p,
 // lane l = (c, h), bf16 element j = W[32 fb + f(8u + j, h)][32 jb + c], f(r, h) = (r & 3) + 8 (r >> 2) + 4 h,
 // w = piece0 + piece1 + piece2 by successive RNE
@@ -534,17 +562,7 @@ static void pack_split_layer(const float* W, int M, uint32_t* dst) {
           for (int j = 0; j < 8; ++j) {
             const int r = 8 * u + j, h = l >> 5;
             const int in = 32 * fb + (r & 3) + 8 * (r >> 2) + 4 * h, out = 32 * jb + (l & 31);
-            const float w = W[(size_t)in * M + out];
-            uint16_t piece[3];
-            piece[0] = bf16_rne(w);
-            const float r1 = w - bf16_float(piece[0]);
-            piece[1] = bf16_rne(r1);
-            const float r2 = r1 - bf16_float(piece[1]);
-            piece[2] = bf16_rne(r2);
-            for (int p = 0; p < 3; ++p) {
-              uint32_t& word = dst[(((size_t)g * 3 + p) * 64 + l) * 4 + (j >> 1)];
-              word = (j & 1) ? ((word & 0x0000ffffu) | ((uint32_t)piece[p] << 16)) : ((word & 0xffff0000u) | piece[p]);
-            }
+            put_split(dst + ((size_t)g * 3 * 64 + l) * 4, 64 * 4, j, W[(size_t)in * M + out]);
           }
       }
 }
@@ -756,7 +774,15 @@ int ecnf_create(const ecnf_cfg* cfg, const float* params, size_t n_floats, int d
 
   // ---- repack ----
   Packer pk;
-  struct Off { size_t Wn, bn, Wp, bp, wd, We, Ws, be, wx, wg, Wh[kMaxPhiH], bh[kMaxPhiH]; float bx, bg; };
+  struct Off {
+    size_t Wn, bn, Wp, bp, wd, We, Ws, be, wx, wg, Wh[kMaxPhiH], bh[kMaxPhiH], Wn_s, Wp_s, Wh_s[kMaxPhiH];
+    float bx, bg;
+  };
+  auto put_split_node = [&](const float* W, int K, int NOUT) {
+    std::vector<uint32_t> v((size_t)(NOUT / 32) * ((K + 15) / 16) * 3 * 64 * 4, 0u);
+    pack_split_node(W, K, NOUT, v.data());
+    return pk.put(reinterpret_cast<const float*>(v.data()), v.size());
+  };
   std::vector<Off> off(K);
   for (int k = 0; k < K; ++k) {
     const HostBlock& b = hb[k];
@@ -771,6 +797,8 @@ int ecnf_create(const ecnf_cfg* cfg, const float* params, size_t n_floats, int d
       }
     for (int j = 0; j < M; ++j) { bp[M + j] = b.eb[0][j]; wd[j] = b.ek[0][(size_t)2 * H * M + j]; }
     o.Wp = pk.put(wp.data(), wp.size());
+    o.Wn_s = put_split_node(b.nk, H + T, H);
+    o.Wp_s = put_split_node(wp.data(), H, 2 * M);
     o.bp = pk.put(bp.data(), bp.size());
     o.wd = pk.put(wd.data(), wd.size());
     // chain: phi_e.1..L-1, phi_x.0..L-1, each [M][M] -> fragment order
@@ -806,6 +834,7 @@ int ecnf_create(const ecnf_cfg* cfg, const float* params, size_t n_floats, int d
     for (int l = 0; l <= L; ++l) {
       const int out_f = l == L ? H : M, in_f = l == 0 ? M + H : M;
       o.Wh[l] = pk.put(b.hk[l], (size_t)in_f * out_f);
+      o.Wh_s[l] = put_split_node(b.hk[l], in_f, out_f);
       o.bh[l] = pk.put(b.hb[l], out_f);
     }
   }
@@ -843,7 +872,13 @@ int ecnf_create(const ecnf_cfg* cfg, const float* params, size_t n_floats, int d
       const Off& o = off[k];
       w.Wn = dbuf + o.Wn; w.bn = dbuf + o.bn; w.Wp = dbuf + o.Wp; w.bp = dbuf + o.bp; w.wd = dbuf + o.wd;
       w.We = dbuf + o.We; w.Ws = reinterpret_cast<const unsigned*>(dbuf + o.Ws); w.be = dbuf + o.be; w.wx = dbuf + o.wx; w.wg = dbuf + o.wg; w.bx = o.bx; w.bg = o.bg;
-      for (int l = 0; l <= L; ++l) { w.Wh[l] = dbuf + o.Wh[l]; w.bh[l] = dbuf + o.bh[l]; }
+      for (int l = 0; l <= L; ++l) {
+        w.Wh[l] = dbuf + o.Wh[l];
+        w.bh[l] = dbuf + o.bh[l];
+        w.Wh_s[l] = reinterpret_cast<const unsigned*>(dbuf + o.Wh_s[l]);
+      }
+      w.Wn_s = reinterpret_cast<const unsigned*>(dbuf + o.Wn_s);
+      w.Wp_s = reinterpret_cast<const unsigned*>(dbuf + o.Wp_s);
     }
     int mpw = 0, rp = 0;
     size_t lds = 0;

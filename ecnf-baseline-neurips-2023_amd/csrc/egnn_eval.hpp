@@ -82,6 +82,8 @@ struct BlockW {
   const float* wx;  const float* wg;    // [M] phi_x output Dense(1) kernel, [M] gate Dense(1) kernel
   float bx, bg;                         // their biases
   const float* Wh[kMaxPhiH]; const float* bh[kMaxPhiH];  // phi_h layers, row-major [in][out]
+  // split-bf16 node GEMM fragments [out block][16-deep k-step][piece][lane] (node_task_split)
+  const unsigned* Wn_s; const unsigned* Wp_s; const unsigned* Wh_s[kMaxPhiH];
 };
 
 struct Net {
@@ -243,6 +245,8 @@ __device__ __forceinline__ void init_bias(f32x16& acc, const float* __restrict__
   }
 }
 
+#include "chain_split.hpp"
+
 // ---------------------------------------------------------------------------------------------------
 // node GEMM k-loop over one source: acc[a] += sum_k W[k][(jb + a)*32 + i] X[n][k] for k in [0, K), NA output
 // blocks sharing every B fragment.  A (global) and B (LDS) fragments are software-pipelined one chunk of CH
@@ -304,24 +308,11 @@ __device__ __forceinline__ void node_kloop(f32x16 (&acc)[NA], f32x16 (&accT)[NA]
   }
 }
 
+// bias/act/residual epilogue of a node GEMM task: Y[n][j] (and the tangent row RP + n)
 template <int NT, int NA>
-__device__ __forceinline__ void node_task(const float* X1, int ldx1, int K1, const float* X2, int ldx2, int K2,
-                                          const float* __restrict__ W, int ldw, const float* __restrict__ bias,
-                                          bool act, const float* resid, int ldr, float* Y, int ldy, int RP,
-                                          int nvalid, int jb, int ct, int lane) {
-  const int kk = lane >> 5, li = lane & 31;
-  const int n = ct * 32 + li;
-  f32x16 acc[NA], accT[NA];
-#pragma unroll
-  for (int a = 0; a < NA; ++a) {
-    init_bias(acc[a], bias, jb + a, kk);
-#pragma unroll
-    for (int r = 0; r < 16; ++r) accT[a][r] = 0.f;
-  }
-  const gfloat_p wcol = gptr(W) + kk * ldw + jb * 32 + li;
-  node_kloop<NT, NA>(acc, accT, wcol, ldw, X1 + n * ldx1 + kk, X1 + (RP + n) * ldx1 + kk, K1);
-  if (K2 > 0)
-    node_kloop<NT, NA>(acc, accT, wcol + K1 * ldw, ldw, X2 + n * ldx2 + kk, X2 + (RP + n) * ldx2 + kk, K2);
+__device__ __forceinline__ void node_epilogue(const f32x16 (&acc)[NA], const f32x16 (&accT)[NA], bool act,
+                                              const float* resid, int ldr, float* Y, int ldy, int RP, int nvalid,
+                                              int jb, int n, int kk) {
   if (n < nvalid) {
 #pragma unroll
     for (int a = 0; a < NA; ++a)
@@ -344,17 +335,138 @@ __device__ __forceinline__ void node_task(const float* X1, int ldx1, int K1, con
   }
 }
 
+template <int NT, int NA>
+__device__ __forceinline__ void node_task(const float* X1, int ldx1, int K1, const float* X2, int ldx2, int K2,
+                                          const float* __restrict__ W, int ldw, const float* __restrict__ bias,
+                                          bool act, const float* resid, int ldr, float* Y, int ldy, int RP,
+                                          int nvalid, int jb, int ct, int lane) {
+  const int kk = lane >> 5, li = lane & 31;
+  const int n = ct * 32 + li;
+  f32x16 acc[NA], accT[NA];
+#pragma unroll
+  for (int a = 0; a < NA; ++a) {
+    init_bias(acc[a], bias, jb + a, kk);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) accT[a][r] = 0.f;
+  }
+  const gfloat_p wcol = gptr(W) + kk * ldw + jb * 32 + li;
+  node_kloop<NT, NA>(acc, accT, wcol, ldw, X1 + n * ldx1 + kk, X1 + (RP + n) * ldx1 + kk, K1);
+  if (K2 > 0)
+    node_kloop<NT, NA>(acc, accT, wcol + K1 * ldw, ldw, X2 + n * ldx2 + kk, X2 + (RP + n) * ldx2 + kk, K2);
+  node_epilogue<NT, NA>(acc, accT, act, resid, ldr, Y, ldy, RP, nvalid, jb, n, kk);
+}
+
+// split-bf16 node GEMM task (primal only): acc[a] = b + sum_k W[k][(jb + a) * 32 + i] X[n][k], the fp32 operands
+// split into three bf16 pieces (six cross terms, chain_split.hpp).  A: host-packed fragments, K zero-padded to
+// a multiple of 16, fetched by buffer loads one k-step ahead; B: the lane's node row, 8 consecutive features
+// from LDS (odd row strides: conflict-free), split in registers; NA output blocks share every B split.
+template <int NA>
+__device__ __forceinline__ void node_task_split(const float* X1, int ldx1, int K1, const float* X2, int ldx2, int K2,
+                                                const unsigned* __restrict__ Wpk, const float* __restrict__ bias,
+                                                bool act, const float* resid, int ldr, float* Y, int ldy, int RP,
+                                                int nvalid, int jb, int ct, int lane) {
+  constexpr int PFA = 2;   // k-steps of A fragments in flight ahead of the MFMAs
+  jb = __builtin_amdgcn_readfirstlane(jb);   // uniform: buffer-load offsets in SGPRs (no waterfall loops)
+  ct = __builtin_amdgcn_readfirstlane(ct);
+  const int kk = lane >> 5, li = lane & 31;
+  const int n = ct * 32 + li;
+  const int nks1 = (K1 + 15) >> 4, nks = nks1 + ((K2 + 15) >> 4);
+  // biases are added in the epilogue: their load latency hides behind the k-loop
+  f32x4 bq[NA][4];
+#pragma unroll
+  for (int a = 0; a < NA; ++a)
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      bq[a][q] = bias ? gptr4(bias + (jb + a) * 32 + 8 * q + 4 * kk)[0] : f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x16 acc[NA], accT[NA];
+#pragma unroll
+  for (int a = 0; a < NA; ++a) acc[a] = f32x16{};
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned*>(Wpk), (short)0,
+                                                                         0x7fffffff, 0x00020000);
+  const int voff = lane * 16;
+  auto bload = [&](int ks, float (&v)[8]) {
+    const bool first = ks < nks1;
+    const float* src = first ? X1 + n * ldx1 : X2 + n * ldx2;
+    const int c0 = 16 * (first ? ks : ks - nks1) + 8 * kk;
+    const int K = first ? K1 : K2;
+    if (c0 + 8 <= K) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = src[c0 + j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (c0 + j < K) ? src[c0 + j] : 0.f;
+    }
+  };
+  auto aload = [&](int ks, u32x4 (&w)[NA][3]) {
+#pragma unroll
+    for (int a = 0; a < NA; ++a)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) w[a][p] = wload(rsrc, voff, (((jb + a) * nks + ks) * 3 + p) * 1024);
+  };
+  float bv[8];
+  u32x4 wa[PFA][NA][3];
+  bload(0, bv);
+#pragma unroll
+  for (int i = 0; i < PFA; ++i)
+    if (i < nks) aload(i, wa[i]);
+  for (int ks = 0; ks < nks; ks += PFA) {
+#pragma unroll
+    for (int i = 0; i < PFA; ++i) {
+      if (ks + i < nks) {
+        u32x4 B[3];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          unsigned p0, p1, p2;
+          split3(bv[2 * e], bv[2 * e + 1], p0, p1, p2);
+          B[0][e] = p0;
+          B[1][e] = p1;
+          B[2][e] = p2;
+        }
+        if (ks + i + 1 < nks) bload(ks + i + 1, bv);
+#pragma unroll
+        for (int a = 0; a < NA; ++a) {
+          acc[a] = mfma_bf16(wa[i][a][2], B[0], acc[a]);
+          acc[a] = mfma_bf16(wa[i][a][1], B[1], acc[a]);
+          acc[a] = mfma_bf16(wa[i][a][0], B[2], acc[a]);
+          acc[a] = mfma_bf16(wa[i][a][1], B[0], acc[a]);
+          acc[a] = mfma_bf16(wa[i][a][0], B[1], acc[a]);
+          acc[a] = mfma_bf16(wa[i][a][0], B[0], acc[a]);
+        }
+        if (ks + i + PFA < nks) aload(ks + i + PFA, wa[i]);
+      }
+    }
+  }
+#pragma unroll
+  for (int a = 0; a < NA; ++a)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[a][r] += bq[a][r >> 2][r & 3];
+  node_epilogue<0, NA>(acc, accT, act, resid, ldr, Y, ldy, RP, nvalid, jb, n, kk);
+}
+
 // ---------------------------------------------------------------------------------------------------
 // node GEMM: Y[n][0:NOUT] = act([X1 | X2][n] W + b) (+ resid[n]); tangent rows RP+n share the A fragments
 // and get no bias, act'(pre) * (X_T W).  Output blocks are paired (shared B reads, two independent MFMA
 // chains) whenever the pairs still give every wave a task.
 // ---------------------------------------------------------------------------------------------------
-template <int NT, int NW>
+template <int NT, int NW, bool SPLIT>
 __device__ __forceinline__ void node_gemm(const float* X1, int ldx1, int K1, const float* X2, int ldx2, int K2,
-                                          const float* __restrict__ W, int ldw, const float* __restrict__ bias,
-                                          int NOUT, bool act, const float* resid, int ldr, float* Y, int ldy,
-                                          int RP, int nvalid, int wave, int lane) {
+                                          const float* __restrict__ W, const unsigned* __restrict__ Ws, int ldw,
+                                          const float* __restrict__ bias, int NOUT, bool act, const float* resid,
+                                          int ldr, float* Y, int ldy, int RP, int nvalid, int wave, int lane) {
   const int njb = NOUT >> 5, nct = RP >> 5;
+  if constexpr (SPLIT) {
+    if ((njb % 2) == 0 && (njb / 2) * nct >= NW) {   // two output blocks per task share the B split
+      const int npair = njb / 2;
+      for (int task = wave; task < npair * nct; task += NW)
+        node_task_split<2>(X1, ldx1, K1, X2, ldx2, K2, Ws, bias, act, resid, ldr, Y, ldy, RP, nvalid,
+                           2 * (task % npair), task / npair, lane);
+    } else {
+      for (int task = wave; task < njb * nct; task += NW)
+        node_task_split<1>(X1, ldx1, K1, X2, ldx2, K2, Ws, bias, act, resid, ldr, Y, ldy, RP, nvalid, task % njb,
+                           task / njb, lane);
+    }
+    return;
+  }
   if (false && (njb % 2) == 0 && (njb / 2) * nct >= NW) {   // pairing measured slower for phi_h (r01)
     const int npair = njb / 2;
     for (int task = wave; task < npair * nct; task += NW)
@@ -484,8 +596,6 @@ __device__ __forceinline__ void chain_segment(f32x16 (&X)[NF], f32x16 (&XT)[NF],
 #pragma unroll
   for (int r = 0; r < 16; ++r) chain_act<NT>(X[NF - 1], XT[NF - 1], acc[NF - 1], accT[NF - 1], r, bb[r >> 2][r & 3]);
 }
-
-#include "chain_split.hpp"
 
 // Segmented (by receiver row) inclusive PREFIX sum over the 32 edge lanes of each half-wave, in DPP:
 // row_shr:1,2,4,8 inside each 16-lane row, then row_bcast:15 carries lane 15's running sum into lanes 16..31
@@ -798,7 +908,9 @@ template <int NF, int NT, int L, int D>
 __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const float* x_in, const float* t_in, const float* tan_in,
                           float* v_out, float* tan_out) {
   constexpr int kNW = Geo<NF, NT>::NW, kNT = Geo<NF, NT>::NTHR;
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  constexpr bool kSplitG = Geo<NF, NT>::kSplit;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: task indices stay in SGPRs
   const int N = net.N, H = net.H, T = net.T, M = NF * 32, RP = net.RP, MPW = net.MPW, ND = net.ND;
   const int nvalid = MPW * N;
   const int R = RP * (1 + NT);
@@ -853,12 +965,12 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
       s.vecs[idx] = val;
     }
     // h <- Dense([h | temb])  (egnn.py:166-167)
-    node_gemm<NT, kNW>(s.hin, s.ld_hin, H + T, nullptr, 0, 0, bw.Wn, H, bw.bn, H, false, nullptr, 0, s.hb, s.ld_hb, RP,
+    node_gemm<NT, kNW, kSplitG>(s.hin, s.ld_hin, H + T, nullptr, 0, 0, bw.Wn, bw.Wn_s, H, bw.bn, H, false, nullptr, 0, s.hb, s.ld_hb, RP,
                   nvalid, wave, lane);
     __syncthreads();
     STAMP(s, kStNodeDense);
     // per-node halves of phi_e layer 1
-    node_gemm<NT, kNW>(s.hb, s.ld_hb, H, nullptr, 0, 0, bw.Wp, 2 * M, bw.bp, 2 * M, false, nullptr, 0, s.P, s.ld_P, RP,
+    node_gemm<NT, kNW, kSplitG>(s.hb, s.ld_hb, H, nullptr, 0, 0, bw.Wp, bw.Wp_s, 2 * M, bw.bp, 2 * M, false, nullptr, 0, s.P, s.ld_P, RP,
                   nvalid, wave, lane);
     __syncthreads();
     STAMP(s, kStPGemm);
@@ -887,7 +999,7 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
     // phi_h = MLP((M,)*L + (H,)) on [m_i | h], residual (egnn.py:105-111)
     float* Q0 = s.P;
     float* Q1 = s.P + (M + 1);
-    node_gemm<NT, kNW>(s.macc, s.ld_m, M, s.hb, s.ld_hb, H, bw.Wh[0], M, bw.bh[0], M, true, nullptr, 0, Q0, s.ld_P, RP,
+    node_gemm<NT, kNW, kSplitG>(s.macc, s.ld_m, M, s.hb, s.ld_hb, H, bw.Wh[0], bw.Wh_s[0], M, bw.bh[0], M, true, nullptr, 0, Q0, s.ld_P, RP,
                   nvalid, wave, lane);
     __syncthreads();
     for (int idx = tid; idx < R * M; idx += kNT) {
@@ -895,12 +1007,12 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
       s.macc[row * s.ld_m + c] = 0.f;
     }
     for (int l = 1; l < L; ++l) {
-      node_gemm<NT, kNW>(Q0, s.ld_P, M, nullptr, 0, 0, bw.Wh[l], M, bw.bh[l], M, true, nullptr, 0, Q1, s.ld_P, RP,
+      node_gemm<NT, kNW, kSplitG>(Q0, s.ld_P, M, nullptr, 0, 0, bw.Wh[l], bw.Wh_s[l], M, bw.bh[l], M, true, nullptr, 0, Q1, s.ld_P, RP,
                     nvalid, wave, lane);
       __syncthreads();
       float* tq = Q0; Q0 = Q1; Q1 = tq;
     }
-    node_gemm<NT, kNW>(Q0, s.ld_P, M, nullptr, 0, 0, bw.Wh[L], H, bw.bh[L], H, false, s.hb, s.ld_hb, s.hin, s.ld_hin, RP,
+    node_gemm<NT, kNW, kSplitG>(Q0, s.ld_P, M, nullptr, 0, 0, bw.Wh[L], bw.Wh_s[L], H, bw.bh[L], H, false, s.hb, s.ld_hb, s.hin, s.ld_hin, RP,
                   nvalid, wave, lane);
     __syncthreads();
     STAMP(s, kStPhiH);

@@ -21,6 +21,9 @@
 #ifndef NWAVES
 #define NWAVES 4
 #endif
+#ifndef LOADSRC
+#define LOADSRC 0   // 0: global (L2/L1), 1: none (fragments stay in registers), 2: LDS
+#endif
 constexpr int kGroups = 32;   // per layer (NF = 4: 4 fb x 2 u x 4 jb)
 constexpr int kLayers = 5;
 constexpr int kTiles = 16;
@@ -59,6 +62,9 @@ __device__ __forceinline__ void act_split(float a0, float a1, float b, unsigned&
 
 __global__ __launch_bounds__(64 * NWAVES) void kern(const unsigned* __restrict__ W, float* out, unsigned long long* cyc) {
   const int lane = threadIdx.x & 63;
+  __shared__ u32x4 lw[8 * 3 * 64];   // 24 KB: 8 groups of fragments
+  for (int i = threadIdx.x; i < 8 * 3 * 64; i += 64 * NWAVES) lw[i] = ((const u32x4*)W)[i];
+  __syncthreads();
   u32x4 X[NS][4][2][3];     // [stream][fb][u][piece]
   f32x16 acc[NS][4];
   for (int s = 0; s < NS; ++s)
@@ -80,8 +86,11 @@ __global__ __launch_bounds__(64 * NWAVES) void kern(const unsigned* __restrict__
       sfor<kGroups>([&](auto Gc) {
         constexpr int g = decltype(Gc)::value;
         constexpr int jb = g & 3, u = (g >> 2) & 1, fb = g >> 3;
-        if constexpr (g + NPF < kGroups) {
+        if constexpr (g + NPF < kGroups && LOADSRC == 0) {
           for (int p = 0; p < 3; ++p) wb[(g + NPF) % (NPF + 1)][p] = wp[((g + NPF) * 3 + p) * 64];
+        }
+        if constexpr (g + NPF < kGroups && LOADSRC == 2) {
+          for (int p = 0; p < 3; ++p) wb[(g + NPF) % (NPF + 1)][p] = lw[((((g + NPF) % 8) * 3 + p) * 64) + lane];
         }
         __builtin_amdgcn_sched_barrier(0);
         const u32x4* A = wb[g % (NPF + 1)];
