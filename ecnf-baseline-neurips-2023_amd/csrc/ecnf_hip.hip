@@ -521,23 +521,51 @@ static inline float bf16_float(uint16_t b) {
   return f;
 }
 
-// w = piece0 + piece1 + piece2 by successive RNE; stores bf16 element j of a lane's 8-element fragment
-static inline void put_split(uint32_t* frag_p0, size_t piece_stride, int j, float w) {
-  uint16_t piece[3];
+// the power-of-two scale s of a split weight matrix (chain_split.hpp): max |w s| in [2^12, 2^13) for fp16 pieces,
+// 1 for bf16 pieces (fp32's exponent range)
+static float split_scale(const float* W, size_t n, size_t ld = 0, size_t cols = 0) {
+#ifdef ECNF_SPLIT_BF16
+  (void)W; (void)n; (void)ld; (void)cols;
+  return 1.0f;
+#else
+  float mx = 0.f;
+  for (size_t i = 0; i < n; ++i) {
+    const float a = std::fabs(ld ? W[(i / cols) * ld + (i % cols)] : W[i]);
+    if (a > mx) mx = a;
+  }
+  if (!(mx > 0.f) || !std::isfinite(mx)) return 1.0f;
+  const int e = std::max(-100, std::min(100, 12 - std::ilogb(mx)));
+  return std::ldexp(1.0f, e);
+#endif
+}
+
+// w s = piece0 + ... by successive RNE; stores 16-bit element j of a lane's 8-element fragment, pieces
+// piece_stride u32 apart
+static inline void put_split(uint32_t* frag_p0, size_t piece_stride, int j, float w, float scale) {
+  uint16_t piece[kPieces];
+#ifdef ECNF_SPLIT_BF16
+  (void)scale;
   piece[0] = bf16_rne(w);
   const float r1 = w - bf16_float(piece[0]);
   piece[1] = bf16_rne(r1);
   const float r2 = r1 - bf16_float(piece[1]);
   piece[2] = bf16_rne(r2);
-  for (int p = 0; p < 3; ++p) {
+#else
+  const float ws = w * scale;   // exact (power of two, no overflow by construction)
+  const _Float16 h0 = (_Float16)ws;
+  const _Float16 h1 = (_Float16)(ws - (float)h0);
+  std::memcpy(&piece[0], &h0, 2);
+  std::memcpy(&piece[1], &h1, 2);
+#endif
+  for (int p = 0; p < kPieces; ++p) {
     uint32_t& word = frag_p0[p * piece_stride + (j >> 1)];
     word = (j & 1) ? ((word & 0x0000ffffu) | ((uint32_t)piece[p] << 16)) : ((word & 0xffff0000u) | piece[p]);
   }
 }
 
-// split-bf16 fragments of a node GEMM W [K][NOUT] (row-major, node_task_split): [out block b][k-step s][piece]
-// [lane l][8 bf16], element j = W[16 s + 8 (l >> 5) + j][32 b + (l & 31)], zero for k >= K
-static void pack_split_node(const float* W, int K, int NOUT, uint32_t* dst) {
+// split fragments of a node GEMM W [K][NOUT] (row-major, node_task_split): [out block b][k-step s][piece]
+// [lane l][8 x 16 bit], element j = W[16 s + 8 (l >> 5) + j][32 b + (l & 31)], zero for k >= K
+static void pack_split_node(const float* W, int K, int NOUT, float scale, uint32_t* dst) {
   const int nks = (K + 15) / 16;
   for (int b = 0; b < NOUT / 32; ++b)
     for (int ks = 0; ks < nks; ++ks)
@@ -545,14 +573,13 @@ static void pack_split_node(const float* W, int K, int NOUT, uint32_t* dst) {
         for (int j = 0; j < 8; ++j) {
           const int k = 16 * ks + 8 * (l >> 5) + j;
           const float w = k < K ? W[(size_t)k * NOUT + 32 * b + (l & 31)] : 0.f;
-          put_split(dst + (((size_t)b * nks + ks) * 3 * 64 + l) * 4, 64 * 4, j, w);
+          put_split(dst + (((size_t)b * nks + ks) * kPieces * 64 + l) * 4, 64 * 4, j, w, scale);
         }
 }
 
-// split-bf16 fragments of one [M][M] chain layer (chain_split.hpp): group g = (jb * NF + fb) * 2 + u, piece p,
-// lane l = (c, h), bf16 element j = W[32 fb + f(8u + j, h)][32 jb + c], f(r, h) = (r & 3) + 8 (r >> 2) + 4 h,
-// w = piece0 + piece1 + piece2 by successive RNE
-static void pack_split_layer(const float* W, int M, uint32_t* dst) {
+// split fragments of one [M][M] chain layer (chain_split.hpp): group g = (jb * NF + fb) * 2 + u, piece p,
+// lane l = (c, h), element j = W[32 fb + f(8u + j, h)][32 jb + c], f(r, h) = (r & 3) + 8 (r >> 2) + 4 h
+static void pack_split_layer(const float* W, int M, float scale, uint32_t* dst) {
   const int NF = M / 32;
   for (int jb = 0; jb < NF; ++jb)
     for (int fb = 0; fb < NF; ++fb)
@@ -562,7 +589,7 @@ static void pack_split_layer(const float* W, int M, uint32_t* dst) {
           for (int j = 0; j < 8; ++j) {
             const int r = 8 * u + j, h = l >> 5;
             const int in = 32 * fb + (r & 3) + 8 * (r >> 2) + 4 * h, out = 32 * jb + (l & 31);
-            put_split(dst + ((size_t)g * 3 * 64 + l) * 4, 64 * 4, j, W[(size_t)in * M + out]);
+            put_split(dst + ((size_t)g * kPieces * 64 + l) * 4, 64 * 4, j, W[(size_t)in * M + out], scale);
           }
       }
 }
@@ -777,10 +804,14 @@ int ecnf_create(const ecnf_cfg* cfg, const float* params, size_t n_floats, int d
   struct Off {
     size_t Wn, bn, Wp, bp, wd, We, Ws, be, wx, wg, Wh[kMaxPhiH], bh[kMaxPhiH], Wn_s, Wp_s, Wh_s[kMaxPhiH];
     float bx, bg;
+    float cinv[2 * 4 - 1], ninv, pinv, hinv[kMaxPhiH];
   };
-  auto put_split_node = [&](const float* W, int K, int NOUT) {
-    std::vector<uint32_t> v((size_t)(NOUT / 32) * ((K + 15) / 16) * 3 * 64 * 4, 0u);
-    pack_split_node(W, K, NOUT, v.data());
+  // packs W [K][NOUT] as split node fragments; returns the offset, *inv = 1 / its scale
+  auto put_split_node = [&](const float* W, int K, int NOUT, float* inv) {
+    std::vector<uint32_t> v((size_t)(NOUT / 32) * ((K + 15) / 16) * kPieces * 64 * 4, 0u);
+    const float sc = split_scale(W, (size_t)K * NOUT);
+    *inv = 1.0f / sc;
+    pack_split_node(W, K, NOUT, sc, v.data());
     return pk.put(reinterpret_cast<const float*>(v.data()), v.size());
   };
   std::vector<Off> off(K);
@@ -797,8 +828,8 @@ int ecnf_create(const ecnf_cfg* cfg, const float* params, size_t n_floats, int d
       }
     for (int j = 0; j < M; ++j) { bp[M + j] = b.eb[0][j]; wd[j] = b.ek[0][(size_t)2 * H * M + j]; }
     o.Wp = pk.put(wp.data(), wp.size());
-    o.Wn_s = put_split_node(b.nk, H + T, H);
-    o.Wp_s = put_split_node(wp.data(), H, 2 * M);
+    o.Wn_s = put_split_node(b.nk, H + T, H, &o.ninv);
+    o.Wp_s = put_split_node(wp.data(), H, 2 * M, &o.pinv);
     o.bp = pk.put(bp.data(), bp.size());
     o.wd = pk.put(wd.data(), wd.size());
     // chain: phi_e.1..L-1, phi_x.0..L-1, each [M][M] -> fragment order
@@ -820,11 +851,16 @@ int ecnf_create(const ecnf_cfg* cfg, const float* params, size_t n_floats, int d
       std::memcpy(be.data() + (size_t)cl * M, bb, M * sizeof(float));
     }
     o.We = pk.put(we.data(), we.size());
-    // the same chain as split-bf16 fragments: [layer][2 NF^2 groups][3 pieces][64 lanes][4 u32]
-    const size_t split_layer = (size_t)2 * NF * NF * 3 * 64 * 4;
+    // the same chain as split fragments: [layer][2 NF^2 groups][kPieces][64 lanes][4 u32]
+    const size_t split_layer = (size_t)2 * NF * NF * kGroupU32;
     std::vector<uint32_t> ws((size_t)nchain * split_layer, 0u);
-    for (int cl = 0; cl < nchain; ++cl)
-      pack_split_layer(cl < L - 1 ? b.ek[cl + 1] : b.tk[cl - (L - 1)], M, ws.data() + cl * split_layer);
+    for (int cl = 0; cl < 2 * 4 - 1; ++cl) o.cinv[cl] = 1.0f;
+    for (int cl = 0; cl < nchain; ++cl) {
+      const float* W = cl < L - 1 ? b.ek[cl + 1] : b.tk[cl - (L - 1)];
+      const float sc = split_scale(W, (size_t)M * M);
+      o.cinv[cl] = 1.0f / sc;
+      pack_split_layer(W, M, sc, ws.data() + cl * split_layer);
+    }
     o.Ws = pk.put(reinterpret_cast<const float*>(ws.data()), ws.size());
     o.be = pk.put(be.data(), be.size());
     o.wx = pk.put(b.xk, M);
@@ -834,7 +870,7 @@ int ecnf_create(const ecnf_cfg* cfg, const float* params, size_t n_floats, int d
     for (int l = 0; l <= L; ++l) {
       const int out_f = l == L ? H : M, in_f = l == 0 ? M + H : M;
       o.Wh[l] = pk.put(b.hk[l], (size_t)in_f * out_f);
-      o.Wh_s[l] = put_split_node(b.hk[l], in_f, out_f);
+      o.Wh_s[l] = put_split_node(b.hk[l], in_f, out_f, &o.hinv[l]);
       o.bh[l] = pk.put(b.hb[l], out_f);
     }
   }
@@ -878,6 +914,10 @@ int ecnf_create(const ecnf_cfg* cfg, const float* params, size_t n_floats, int d
         w.Wh_s[l] = reinterpret_cast<const unsigned*>(dbuf + o.Wh_s[l]);
       }
       w.Wn_s = reinterpret_cast<const unsigned*>(dbuf + o.Wn_s);
+      for (int cl = 0; cl < 2 * 4 - 1; ++cl) w.cinv[cl] = o.cinv[cl];
+      w.ninv = o.ninv;
+      w.pinv = o.pinv;
+      for (int l = 0; l <= L; ++l) w.hinv[l] = o.hinv[l];
       w.Wp_s = reinterpret_cast<const unsigned*>(dbuf + o.Wp_s);
     }
     int mpw = 0, rp = 0;
@@ -919,7 +959,11 @@ int ecnf_molecules_per_workgroup(ecnf_handle* h, int32_t with_tangent, int32_t* 
 int ecnf_chain_arithmetic(ecnf_handle* h, int32_t with_tangent, int32_t* mode) {
   if (!h || !mode) return fail(ECNF_E_INVALID, "NULL argument");
   const bool split = kSplitChain && !with_tangent && h->cfg.mlp_width <= 128;   // Geo<NF, NT>::kSplit
+#ifdef ECNF_SPLIT_BF16
   *mode = split ? ECNF_CHAIN_SPLIT_BF16 : ECNF_CHAIN_FP32_MFMA;
+#else
+  *mode = split ? ECNF_CHAIN_SPLIT_F16 : ECNF_CHAIN_FP32_MFMA;
+#endif
   return ECNF_OK;
 }
 

@@ -82,8 +82,11 @@ struct BlockW {
   const float* wx;  const float* wg;    // [M] phi_x output Dense(1) kernel, [M] gate Dense(1) kernel
   float bx, bg;                         // their biases
   const float* Wh[kMaxPhiH]; const float* bh[kMaxPhiH];  // phi_h layers, row-major [in][out]
-  // split-bf16 node GEMM fragments [out block][16-deep k-step][piece][lane] (node_task_split)
+  // split node GEMM fragments [out block][16-deep k-step][piece][lane] (node_task_split)
   const unsigned* Wn_s; const unsigned* Wp_s; const unsigned* Wh_s[kMaxPhiH];
+  // 1 / the power-of-two scale of each split weight matrix (chain_split.hpp): chain layers, Wn, Wp, phi_h
+  float cinv[2 * 4 - 1];
+  float ninv, pinv, hinv[kMaxPhiH];
 };
 
 struct Net {
@@ -362,8 +365,8 @@ __device__ __forceinline__ void node_task(const float* X1, int ldx1, int K1, con
 // from LDS (odd row strides: conflict-free), split in registers; NA output blocks share every B split.
 template <int NA>
 __device__ __forceinline__ void node_task_split(const float* X1, int ldx1, int K1, const float* X2, int ldx2, int K2,
-                                                const unsigned* __restrict__ Wpk, const float* __restrict__ bias,
-                                                bool act, const float* resid, int ldr, float* Y, int ldy, int RP,
+                                                const unsigned* __restrict__ Wpk, float winv,
+                                                const float* __restrict__ bias, bool act, const float* resid, int ldr, float* Y, int ldy, int RP,
                                                 int nvalid, int jb, int ct, int lane) {
   constexpr int PFA = 2;   // k-steps of A fragments in flight ahead of the MFMAs
   jb = __builtin_amdgcn_readfirstlane(jb);   // uniform: buffer-load offsets in SGPRs (no waterfall loops)
@@ -397,14 +400,14 @@ __device__ __forceinline__ void node_task_split(const float* X1, int ldx1, int K
       for (int j = 0; j < 8; ++j) v[j] = (c0 + j < K) ? src[c0 + j] : 0.f;
     }
   };
-  auto aload = [&](int ks, u32x4 (&w)[NA][3]) {
+  auto aload = [&](int ks, u32x4 (&w)[NA][kPieces]) {
 #pragma unroll
     for (int a = 0; a < NA; ++a)
 #pragma unroll
-      for (int p = 0; p < 3; ++p) w[a][p] = wload(rsrc, voff, (((jb + a) * nks + ks) * 3 + p) * 1024);
+      for (int p = 0; p < kPieces; ++p) w[a][p] = wload(rsrc, voff, (((jb + a) * nks + ks) * kPieces + p) * kPieceBytes);
   };
   float bv[8];
-  u32x4 wa[PFA][NA][3];
+  u32x4 wa[PFA][NA][kPieces];
   bload(0, bv);
 #pragma unroll
   for (int i = 0; i < PFA; ++i)
@@ -413,25 +416,21 @@ __device__ __forceinline__ void node_task_split(const float* X1, int ldx1, int K
 #pragma unroll
     for (int i = 0; i < PFA; ++i) {
       if (ks + i < nks) {
-        u32x4 B[3];
+        u32x4 B[kPieces];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          unsigned p0, p1, p2;
-          split3(bv[2 * e], bv[2 * e + 1], p0, p1, p2);
-          B[0][e] = p0;
-          B[1][e] = p1;
-          B[2][e] = p2;
+          unsigned pc[kPieces];
+          split_pair(bv[2 * e], bv[2 * e + 1], pc);
+#pragma unroll
+          for (int p = 0; p < kPieces; ++p) B[p][e] = pc[p];
         }
         if (ks + i + 1 < nks) bload(ks + i + 1, bv);
 #pragma unroll
-        for (int a = 0; a < NA; ++a) {
-          acc[a] = mfma_bf16(wa[i][a][2], B[0], acc[a]);
-          acc[a] = mfma_bf16(wa[i][a][1], B[1], acc[a]);
-          acc[a] = mfma_bf16(wa[i][a][0], B[2], acc[a]);
-          acc[a] = mfma_bf16(wa[i][a][1], B[0], acc[a]);
-          acc[a] = mfma_bf16(wa[i][a][0], B[1], acc[a]);
-          acc[a] = mfma_bf16(wa[i][a][0], B[0], acc[a]);
-        }
+        for (int a = 0; a < NA; ++a)
+          static_for<kTerms>([&](auto Tc) {
+            constexpr int t = decltype(Tc)::value;
+            acc[a] = mfma_split(wa[i][a][term_w(t)], B[term_x(t)], acc[a]);
+          });
         if (ks + i + PFA < nks) aload(ks + i + PFA, wa[i]);
       }
     }
@@ -439,7 +438,7 @@ __device__ __forceinline__ void node_task_split(const float* X1, int ldx1, int K
 #pragma unroll
   for (int a = 0; a < NA; ++a)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[a][r] += bq[a][r >> 2][r & 3];
+    for (int r = 0; r < 16; ++r) acc[a][r] = fmaf(acc[a][r], winv, bq[a][r >> 2][r & 3]);
   node_epilogue<0, NA>(acc, accT, act, resid, ldr, Y, ldy, RP, nvalid, jb, n, kk);
 }
 
@@ -450,19 +449,19 @@ __device__ __forceinline__ void node_task_split(const float* X1, int ldx1, int K
 // ---------------------------------------------------------------------------------------------------
 template <int NT, int NW, bool SPLIT>
 __device__ __forceinline__ void node_gemm(const float* X1, int ldx1, int K1, const float* X2, int ldx2, int K2,
-                                          const float* __restrict__ W, const unsigned* __restrict__ Ws, int ldw,
-                                          const float* __restrict__ bias, int NOUT, bool act, const float* resid,
+                                          const float* __restrict__ W, const unsigned* __restrict__ Ws, float winv,
+                                          int ldw, const float* __restrict__ bias, int NOUT, bool act, const float* resid,
                                           int ldr, float* Y, int ldy, int RP, int nvalid, int wave, int lane) {
   const int njb = NOUT >> 5, nct = RP >> 5;
   if constexpr (SPLIT) {
     if ((njb % 2) == 0 && (njb / 2) * nct >= NW) {   // two output blocks per task share the B split
       const int npair = njb / 2;
       for (int task = wave; task < npair * nct; task += NW)
-        node_task_split<2>(X1, ldx1, K1, X2, ldx2, K2, Ws, bias, act, resid, ldr, Y, ldy, RP, nvalid,
+        node_task_split<2>(X1, ldx1, K1, X2, ldx2, K2, Ws, winv, bias, act, resid, ldr, Y, ldy, RP, nvalid,
                            2 * (task % npair), task / npair, lane);
     } else {
       for (int task = wave; task < njb * nct; task += NW)
-        node_task_split<1>(X1, ldx1, K1, X2, ldx2, K2, Ws, bias, act, resid, ldr, Y, ldy, RP, nvalid, task % njb,
+        node_task_split<1>(X1, ldx1, K1, X2, ldx2, K2, Ws, winv, bias, act, resid, ldr, Y, ldy, RP, nvalid, task % njb,
                            task / njb, lane);
     }
     return;
@@ -838,7 +837,13 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
     STAMP_LANE0(s, kStEdgeLayer1, t_sub);
     // phi_e layers 2..L
     const unsigned* Ws = launder_uniform(bw.Ws);
-    chain_split<NF, L - 1>(XA, XB, acc, Ws, s.vecs, lane);
+    ChainInv ie, ix;
+    static_for<2 * 4 - 1>([&](auto Lc) {
+      constexpr int l = decltype(Lc)::value;
+      ie.v[l] = l < L - 1 ? bw.cinv[l] : 1.0f;
+      ix.v[l] = l < L ? bw.cinv[L - 1 + l] : 1.0f;
+    });
+    chain_split<NF, L - 1>(XA, XB, acc, Ws, s.vecs, ie, lane);
     STAMP_LANE0(s, kStEdgeChainE, t_sub);
     edge_tail<NF, NT, L, D>(net, bw, s, acc, acc, valid, rr, r, dr, length, dlength, lane,
                             [&](f32x16 (&m)[NF], f32x16 (&)[NF]) {
@@ -850,8 +855,8 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
                                   put_pair<NF, fb, 2 * i>(XA, m[fb][2 * i], m[fb][2 * i + 1]);
                                 });
                               });
-                              const unsigned* Wx = launder_uniform(bw.Ws + (size_t)(L - 1) * SplitPlan<NF>::GL * 768);
-                              chain_split<NF, L>(XA, XB, m, Wx, s.vecs + (L - 1) * NF * 32, lane);
+                              const unsigned* Wx = launder_uniform(bw.Ws + (size_t)(L - 1) * SplitPlan<NF>::GL * kGroupU32);
+                              chain_split<NF, L>(XA, XB, m, Wx, s.vecs + (L - 1) * NF * 32, ix, lane);
                             });
     STAMP_LANE0(s, kStEdgeTail, t_sub);
     return;
@@ -965,12 +970,12 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
       s.vecs[idx] = val;
     }
     // h <- Dense([h | temb])  (egnn.py:166-167)
-    node_gemm<NT, kNW, kSplitG>(s.hin, s.ld_hin, H + T, nullptr, 0, 0, bw.Wn, bw.Wn_s, H, bw.bn, H, false, nullptr, 0, s.hb, s.ld_hb, RP,
+    node_gemm<NT, kNW, kSplitG>(s.hin, s.ld_hin, H + T, nullptr, 0, 0, bw.Wn, bw.Wn_s, bw.ninv, H, bw.bn, H, false, nullptr, 0, s.hb, s.ld_hb, RP,
                   nvalid, wave, lane);
     __syncthreads();
     STAMP(s, kStNodeDense);
     // per-node halves of phi_e layer 1
-    node_gemm<NT, kNW, kSplitG>(s.hb, s.ld_hb, H, nullptr, 0, 0, bw.Wp, bw.Wp_s, 2 * M, bw.bp, 2 * M, false, nullptr, 0, s.P, s.ld_P, RP,
+    node_gemm<NT, kNW, kSplitG>(s.hb, s.ld_hb, H, nullptr, 0, 0, bw.Wp, bw.Wp_s, bw.pinv, 2 * M, bw.bp, 2 * M, false, nullptr, 0, s.P, s.ld_P, RP,
                   nvalid, wave, lane);
     __syncthreads();
     STAMP(s, kStPGemm);
@@ -999,7 +1004,7 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
     // phi_h = MLP((M,)*L + (H,)) on [m_i | h], residual (egnn.py:105-111)
     float* Q0 = s.P;
     float* Q1 = s.P + (M + 1);
-    node_gemm<NT, kNW, kSplitG>(s.macc, s.ld_m, M, s.hb, s.ld_hb, H, bw.Wh[0], bw.Wh_s[0], M, bw.bh[0], M, true, nullptr, 0, Q0, s.ld_P, RP,
+    node_gemm<NT, kNW, kSplitG>(s.macc, s.ld_m, M, s.hb, s.ld_hb, H, bw.Wh[0], bw.Wh_s[0], bw.hinv[0], M, bw.bh[0], M, true, nullptr, 0, Q0, s.ld_P, RP,
                   nvalid, wave, lane);
     __syncthreads();
     for (int idx = tid; idx < R * M; idx += kNT) {
@@ -1007,12 +1012,12 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
       s.macc[row * s.ld_m + c] = 0.f;
     }
     for (int l = 1; l < L; ++l) {
-      node_gemm<NT, kNW, kSplitG>(Q0, s.ld_P, M, nullptr, 0, 0, bw.Wh[l], bw.Wh_s[l], M, bw.bh[l], M, true, nullptr, 0, Q1, s.ld_P, RP,
+      node_gemm<NT, kNW, kSplitG>(Q0, s.ld_P, M, nullptr, 0, 0, bw.Wh[l], bw.Wh_s[l], bw.hinv[l], M, bw.bh[l], M, true, nullptr, 0, Q1, s.ld_P, RP,
                     nvalid, wave, lane);
       __syncthreads();
       float* tq = Q0; Q0 = Q1; Q1 = tq;
     }
-    node_gemm<NT, kNW, kSplitG>(Q0, s.ld_P, M, nullptr, 0, 0, bw.Wh[L], bw.Wh_s[L], H, bw.bh[L], H, false, s.hb, s.ld_hb, s.hin, s.ld_hin, RP,
+    node_gemm<NT, kNW, kSplitG>(Q0, s.ld_P, M, nullptr, 0, 0, bw.Wh[L], bw.Wh_s[L], bw.hinv[L], H, bw.bh[L], H, false, s.hb, s.ld_hb, s.hin, s.ld_hin, RP,
                   nvalid, wave, lane);
     __syncthreads();
     STAMP(s, kStPhiH);

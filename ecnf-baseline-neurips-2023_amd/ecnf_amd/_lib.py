@@ -15,7 +15,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 ECNF_OK, ECNF_E_INVALID, ECNF_E_UNSUPPORTED, ECNF_E_HIP, ECNF_E_MAX_STEPS = 0, 1, 2, 3, 4
 SOLVER_EULER, SOLVER_DOPRI5 = 0, 1
 DIV_NONE, DIV_HUTCHINSON, DIV_EXACT = 0, 1, 2
-CHAIN_FP32_MFMA, CHAIN_SPLIT_BF16 = 0, 1
+CHAIN_FP32_MFMA, CHAIN_SPLIT_BF16, CHAIN_SPLIT_F16 = 0, 1, 2
 
 # every symbol include/ecnf.h declares
 EXPORTED_SYMBOLS = (

@@ -118,10 +118,11 @@ class EcnfHandle:
         return v.value
 
     def chain_arithmetic(self, with_tangent: bool = False) -> str:
-        """'split_bf16' (fp32-accurate 3-piece bf16 split, chain_split.hpp) or 'fp32_mfma'."""
+        """'split_f16' (2-piece fp16 split, 3 cross terms), 'split_bf16' (3-piece bf16 split, 6 cross terms; both
+        chain_split.hpp) or 'fp32_mfma'."""
         v = ctypes.c_int32()
         _lib.check(self.lib.ecnf_chain_arithmetic(self._h, int(with_tangent), ctypes.byref(v)))
-        return "split_bf16" if v.value == _lib.CHAIN_SPLIT_BF16 else "fp32_mfma"
+        return {_lib.CHAIN_SPLIT_BF16: "split_bf16", _lib.CHAIN_SPLIT_F16: "split_f16"}.get(v.value, "fp32_mfma")
 
     # ---------------------------------------------------------------------------------- C-ABI calls
     def vector_field(self, x, t, feat) -> torch.Tensor:

@@ -3,8 +3,9 @@
 Tolerances (fp32 kernel vs fp64 oracle; stated per test):
   * one vector-field evaluation / JVP: max |err| <= 2e-5 * max(1, max |ref|)
   * fixed-step trajectories (100 Euler steps, 20 Dopri5 steps): max |err| <= 1e-4
-  * adaptive Dopri5: step sequences fork in fp32, so the kernel must be within 2x the oracle's own distance to an
-    accurate fp64 fixed-step solution, batch-mean NFE within 30 % of the oracle's
+  * adaptive Dopri5: step sequences fork in fp32, so the kernel must be within 2x the largest distance of the
+    oracle's own fp32 adaptive solves (x0 and 1e-7-perturbed copies) to an accurate fp64 fixed-step solution,
+    batch-mean NFE within 30 % of the oracle's
   * log-densities: |err| <= 2e-3 absolute (values are O(10-100))
 """
 import numpy as np
@@ -170,19 +171,33 @@ def test_dopri5_fixed_sample():
     assert (nfe.cpu().numpy() == 121).all() and (nfe_ref == 121).all()
 
 
-@pytest.mark.parametrize("name", ["dw4", "aldp"])
-def test_dopri5_adaptive_sample(name):
-    """PIDController(rtol=atol=1e-5) solves fork in their accept/reject sequences under fp32 rounding, so the
-    kernel is held to the accuracy of the oracle's own adaptive solve: both are compared to an accurate
-    fixed-step fp64 solution (Dopri5, dt = 0.005) and the kernel may be at most 2x (+2e-4) further from it;
-    the batch-mean NFE must lie within 30 % of the oracle's."""
+def _perturbed(x0, k):
+    """x0 with a relative 1e-7 (fp32 rounding-size) perturbation, seed k (k = 0: x0 itself)."""
+    if k == 0:
+        return x0
+    return (x0 * (1 + 1e-7 * np.random.default_rng(100 + k).standard_normal(x0.shape))).astype(np.float32)
+
+
+@pytest.mark.parametrize("name,n_pert", [("dw4", 3), ("aldp", 1)])
+def test_dopri5_adaptive_sample(name, n_pert):
+    """PIDController(rtol=atol=1e-5) solves fork in their accept/reject sequences under fp32 rounding: 1e-7
+    relative input perturbations move the oracle's own fp32 adaptive solution for one DW4 molecule between
+    7e-5 and 3e-3 from an accurate fp64 fixed-step solution (Dopri5, dt = 0.005).  The kernel is held to that
+    envelope: its distance to the fp64 solution may be at most 2x (+2e-4) the largest distance among the oracle's
+    fp32 adaptive solves of x0 and n_pert perturbed copies; the batch-mean NFE must lie within 30 % of the
+    oracle's."""
     cfg = CONFIGS[name]
     oc, params, h, z, x0, feat = setup(cfg, B=5)
     y1, _, nfe, _ = h.integrate(g(x0), g(feat, torch.int32), 0.0, 1.0, SolveOptions("dopri5", None))
-    ref, nfe_ref = O.sample_cnf(params, oc, x0, feat, solver="dopri5", dt0=None, dtype=np.float32)
     fine, _ = O.sample_cnf(params, oc, x0, feat, solver="dopri5", dt0=0.005, dtype=np.float64)
+    err_o = 0.0
+    for k in range(n_pert + 1):
+        ref_k, nfe_k = O.sample_cnf(params, oc, _perturbed(x0, k), feat, solver="dopri5", dt0=None,
+                                    dtype=np.float32)
+        err_o = max(err_o, float(np.abs(ref_k - fine).max()))
+        if k == 0:
+            nfe_ref = nfe_k
     err_k = np.abs(y1.cpu().numpy() - fine).max()
-    err_o = np.abs(ref - fine).max()
     assert err_k <= 2 * err_o + 2e-4, (err_k, err_o)
     # per-molecule step counts are chaotic under 1e-7 input perturbations (the oracle's own NFE for one ALDP
     # molecule spans 147-309), so the NFE check is on the batch mean

@@ -1,4 +1,4 @@
-// The production split-bf16 chain (chain_split.hpp) in isolation: 4 waves/CU, each runs TILES x (2-layer + 3-layer
+// The production split chain (chain_split.hpp) in isolation: 4 waves/CU, each runs TILES x (2-layer + 3-layer
 // segments) on synthetic activations with the real weight packing size and LDS biases.  Cycles per layer.
 #include "../../ecnf-baseline-neurips-2023_amd/csrc/egnn_eval.hpp"
 #include <cstdio>
@@ -8,7 +8,7 @@ using namespace ecnf;
 #define TILES 16
 #endif
 constexpr int NF = 4, M = 128;
-constexpr size_t kLayerU32 = (size_t)2 * NF * NF * 3 * 64 * 4;
+constexpr size_t kLayerU32 = (size_t)2 * NF * NF * kGroupU32;
 
 __global__ __launch_bounds__(256) void kern(const unsigned* __restrict__ W, const float* __restrict__ b, float* out,
                                             unsigned long long* cyc) {
@@ -20,10 +20,12 @@ __global__ __launch_bounds__(256) void kern(const unsigned* __restrict__ W, cons
   f32x16 acc[NF];
   for (int f = 0; f < NF; ++f)
     for (int u = 0; u < 2; ++u)
-      for (int p = 0; p < 3; ++p) XA.v[f][u][p] = u32x4{0x3f803f80u + lane, 0x3f00u + f, 0x3e803e80u + u, 0x3c003c00u + p};
+      for (int p = 0; p < kPieces; ++p) XA.v[f][u][p] = u32x4{0x3f803f80u + lane, 0x3f00u + f, 0x3e803e80u + u, 0x3c003c00u + p};
+  ChainInv inv;
+  for (int l = 0; l < 7; ++l) inv.v[l] = 1.0f / 4096;
   unsigned long long t0 = __builtin_amdgcn_s_memtime();
   for (int t = 0; t < TILES; ++t) {
-    chain_split<NF, 2>(XA, XB, acc, launder_uniform(W), bias, lane);
+    chain_split<NF, 2>(XA, XB, acc, launder_uniform(W), bias, inv, lane);
     static_for<NF>([&](auto Fc) {
       constexpr int fb = decltype(Fc)::value;
       static_for<8>([&](auto Ic) {
@@ -31,7 +33,7 @@ __global__ __launch_bounds__(256) void kern(const unsigned* __restrict__ W, cons
         put_pair<NF, fb, 2 * i>(XA, acc[fb][2 * i], acc[fb][2 * i + 1]);
       });
     });
-    chain_split<NF, 3>(XA, XB, acc, launder_uniform(W + 2 * kLayerU32), bias + 2 * M, lane);
+    chain_split<NF, 3>(XA, XB, acc, launder_uniform(W + 2 * kLayerU32), bias + 2 * M, inv, lane);
     static_for<NF>([&](auto Fc) {
       constexpr int fb = decltype(Fc)::value;
       static_for<8>([&](auto Ic) {
@@ -68,7 +70,7 @@ int main() {
     float ms; (void)hipEventElapsedTime(&ms, e0, e1);
     (void)hipMemcpy(hc.data(), cyc, 256 * 4 * 8, hipMemcpyDeviceToHost);
     double m = 0; for (auto c : hc) m += c; m /= hc.size();
-    if (rep == 3) printf("split chain: %.0f cycles/layer (ideal %d), %.3f ms\n", m / (TILES * 5.0), 32 * 6 * 32, ms);
+    if (rep == 3) printf("split chain: %.0f cycles/layer (MFMA-bound %d), %.3f ms\n", m / (TILES * 5.0), 32 * kTerms * 32, ms);
   }
   return 0;
 }
