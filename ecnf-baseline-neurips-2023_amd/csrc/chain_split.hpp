@@ -94,6 +94,16 @@ __device__ __forceinline__ void split_pair(float y0, float y1, unsigned (&p)[kPi
 #endif
 }
 
+// SiLU in the log2 domain.  The split kernels carry every pre-activation as u = -log2(e) t (the host folds the
+// factor into the biases and the first layer's weights) and every activation as y' = -log2(e) silu(t):
+//   y' = u / (1 + 2^u)
+// (v_exp_f32, v_add, v_rcp_f32, v_mul).  A layer fed y' needs no change of its weights: W y + b = -ln2 W y' + b,
+// so u_next = W y' - log2(e) b.  The consumers of a chain's last layer (gate and phi_x-output vectors, the message
+// aggregate) take the -ln 2 on the host / in the node update.
+__device__ __forceinline__ float silu_u(float u) {
+  return u * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(u));
+}
+
 // store elements (r, r+1) of block j (accumulator register order) into split buffer X
 template <int NF, int J, int R>
 __device__ __forceinline__ void put_pair(SplitX<NF>& X, float y0, float y1) {
@@ -105,68 +115,77 @@ __device__ __forceinline__ void put_pair(SplitX<NF>& X, float y0, float y1) {
   for (int i = 0; i < kPieces; ++i) X.v[J][u][i][w] = p[i];
 }
 
-template <int NF>
+// The activation of a layer's output block runs as a 3-stage software pipeline across MFMA groups, so the VALU that
+// fills each MFMA gap has no dependency on the VALU of the same gap (no transcendental-latency stalls):
+//   stage A (group gA): u = acc inv + b'; e = 2^u          (v_fma, v_exp)
+//   stage B (group gB): r = 1 / (1 + e)                      (v_add, v_rcp)
+//   stage C (group gC): y' = u r, split into the next layer's input buffer (v_mul, v_cvt_pk, 2 v_fma_mix), or kept
+//                       fp32 in place in acc for the segment's last layer
+// An item is one pair of elements (rows 2p, 2p+1 of the accumulator registers) of output block j of layer l.
+// Groups are output-block major: block jb of a layer accumulates in groups [jb GB, (jb + 1) GB), GB = 2 NF.
+// Constraints per item: gA after the block's last MFMA group; gA before layer l+1 re-zeroes acc[j] (group
+// (l+1) GL + j GB); gC before layer l+1 first reads input block j (group (l+1) GL + 2 j).  Items spread evenly
+// over that window, gB = gA + 1, gC = gA + 2 where the window allows (compressed into fewer groups otherwise).
+template <int NF, int NL>
 struct SplitPlan {
   static constexpr int GB = 2 * NF;        // groups per output block
   static constexpr int GL = NF * GB;       // groups per layer
-  // groups of the next layer available to the last block: its split (stage 2) runs one group after its SiLU
-  // (stage 1) and must land before group (jb 0, fb NF-1) reads it
-  static constexpr int WIN = 2 * NF - 3 > 0 ? 2 * NF - 3 : 1;
-  // activation work of group g of a layer: {block, layer offset, first pair, end pair}; block -1 = none.
-  // pairs are 0..7 (16 elements of a block)
-  struct Task { int j, dl, p0, p1; };
-  static constexpr Task task(int g, bool has_prev) {
-    const int jb = g / GB, k = g % GB;
-    // block jb-1 during the first GB-1 groups of block jb (its stage 2 then lands inside this layer)
-    if (jb >= 1) return k < GB - 1 ? Task{jb - 1, 0, (8 * k) / (GB - 1), (8 * (k + 1)) / (GB - 1)} : Task{-1, 0, 0, 0};
-    if (has_prev && k < WIN) return Task{NF - 1, -1, (8 * k) / WIN, (8 * (k + 1)) / WIN};
-    return Task{-1, 0, 0, 0};
+  static constexpr int G = NL * GL;        // MFMA groups of the segment
+  static constexpr int PPB = 8;            // element pairs per block (16 accumulator registers)
+  static constexpr int NI = NL * NF * PPB; // items
+  struct Item { int l, j, p, gA, gB, gC; };
+  static constexpr int imin(int a, int b) { return a < b ? a : b; }
+  static constexpr int imax(int a, int b) { return a > b ? a : b; }
+  static constexpr Item item(int id) {
+    const int l = id / (NF * PPB), j = (id / PPB) % NF, p = id % PPB;
+    const int base = l * GL + (j + 1) * GB;                 // first group after the block's last MFMA
+    const int deadline = (l + 1) * GL + 2 * j - 1;          // last group that may still write input block j
+    const int span = imax(1, deadline - base - 1);          // groups with room for gC = gA + 2
+    const int rate = (PPB + span - 1) / span;               // items per stage-A group
+    const int gA = base + p / rate;
+    const int gC = imax(gA, imin(gA + 2, deadline));
+    const int gB = imin(gA + 1, gC);
+    return Item{l, j, p, gA, gB, gC};
   }
-  // MFMA slot (1..5 of the group's 6) after which pair number i of n is issued
-  static constexpr int slot(int i, int n) { return 1 + (i * 5) / (n > 0 ? n : 1); }
+  static constexpr int last_group() {
+    int m = G - 1;
+    for (int i = 0; i < NI; ++i) m = imax(m, item(i).gC);
+    return m;
+  }
+  // number of items with stage S (0 = A, 1 = B, 2 = C) in group g, and the id of the k-th one
+  static constexpr int stage_g(const Item& it, int S) { return S == 0 ? it.gA : S == 1 ? it.gB : it.gC; }
+  static constexpr int count(int g, int S) {
+    int n = 0;
+    for (int i = 0; i < NI; ++i) n += stage_g(item(i), S) == g;
+    return n;
+  }
+  static constexpr int nth(int g, int S, int k) {
+    for (int i = 0; i < NI; ++i)
+      if (stage_g(item(i), S) == g && k-- == 0) return i;
+    return -1;
+  }
+  // LDS address (floats, lane half 0) of the two biases of item id; the lane half adds 4
+  static constexpr int bias_off(int id) {
+    const Item it = item(id);
+    const int r = 2 * it.p;
+    return it.l * NF * 32 + it.j * 32 + 8 * (r >> 2) + (r & 3);
+  }
 };
 
-// element pair activation: y = silu(acc + b) (Dense then SiLU, mlp.py:14), either split into X or fp32 in place;
-// b2 = the biases of rows (R, R+1), inv = 1 / (the layer's weight scale)
-template <int NF, int J, int R, bool SPLIT>
-__device__ __forceinline__ void act_pair(f32x16 (&acc)[NF], SplitX<NF>& X, f32x2 b2, float inv) {
-#ifdef ECNF_SPLIT_CHEAP_ACT   // timing experiment: keep the data flow, drop the arithmetic
-  if constexpr (SPLIT) {
-    X.v[J][R >> 3][0][(R & 7) >> 1] = __builtin_bit_cast(unsigned, acc[J][R]);
-    X.v[J][R >> 3][1][(R & 7) >> 1] = __builtin_bit_cast(unsigned, acc[J][R + 1]);
-  }
-  return;
-#endif
-  const float t0 = fmaf(acc[J][R], inv, b2[0]);
-  const float t1 = fmaf(acc[J][R + 1], inv, b2[1]);
-  const float y0 = t0 * sigmoidf_(t0);
-  const float y1 = t1 * sigmoidf_(t1);
-  if constexpr (SPLIT) {
-#ifdef ECNF_SPLIT_NO_SPLIT
-    X.v[J][R >> 3][0][(R & 7) >> 1] = __builtin_bit_cast(unsigned, y0) ^ __builtin_bit_cast(unsigned, y1);
-#else
-    put_pair<NF, J, R>(X, y0, y1);
-#endif
-  } else {
-    acc[J][R] = y0;
-    acc[J][R + 1] = y1;
-  }
-}
+// per-layer 1 / weight scale of a chain segment (wave-uniform)
+struct ChainInv {
+  float v[2 * 4 - 1];
+};
 
-// the activation in two stages, one group apart (software pipelined for ILP):
-//   stage 1: y = silu(acc + b) -> y2 (kept fp32 in place in acc for the final layer)
-//   stage 2: split y2 into the three bf16 pieces of the next layer's input
-template <int NF, int J, int R, bool SPLIT>
-__device__ __forceinline__ f32x2 act_stage1(f32x16 (&acc)[NF], f32x2 b2, float inv) {
-  const float t0 = fmaf(acc[J][R], inv, b2[0]);
-  const float t1 = fmaf(acc[J][R + 1], inv, b2[1]);
-  const float y0 = t0 * sigmoidf_(t0);
-  const float y1 = t1 * sigmoidf_(t1);
-  if constexpr (!SPLIT) {
-    acc[J][R] = y0;
-    acc[J][R + 1] = y1;
-  }
-  return f32x2{y0, y1};
+#ifndef ECNF_SPLIT_PF
+#define ECNF_SPLIT_PF 3
+#endif
+
+__device__ __forceinline__ u32x4 wload(__amdgpu_buffer_rsrc_t rsrc, int voff, int soff) {
+#ifdef ECNF_SPLIT_WLOAD_SAME   // timing experiment: every group reads the first group's fragments (L1-resident)
+  soff &= 2047;
+#endif
+  return __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, soff, 0);
 }
 
 template <int I, typename A, typename B>
@@ -174,138 +193,136 @@ __device__ __forceinline__ auto& pick(A& a, B& b) {
   if constexpr (I == 0) return a; else return b;
 }
 
-#ifndef ECNF_SPLIT_PF
-#define ECNF_SPLIT_PF 3
-#endif
-
-__device__ __forceinline__ u32x4 wload(__amdgpu_buffer_rsrc_t rsrc, int voff, int soff) {
-  return __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, soff, 0);
-}
-
-// per-layer 1 / weight scale of a chain segment (wave-uniform)
-struct ChainInv {
-  float v[2 * 4 - 1];
-};
-
 // NL chained layers Y = silu(X W_l + b_l).  Input in XA (split form); on return acc holds the last layer's
-// activations in fp32 (accumulator layout).  XA / XB are both clobbered.
+// activations y' (log2 domain, silu_u) in fp32 (accumulator layout).  XA / XB are both clobbered.
 // Weights: packed split fragments [layer][group][piece][lane] (16 B), read as buffer loads with the group
-// offset in an SGPR; biases: LDS [NL][M], each activated pair's two (adjacent) rows read one group ahead;
-// inv.v[l]: 1 / the weight scale of layer l.
-// Each group's MFMAs and activation VALU are emitted together and interleaved by sched_group_barrier: the
-// weight loads first, then MFMA / VALU alternately, so the VALU fills the MFMAs' free issue cycles.
+// offset in an SGPR, PF groups ahead; biases: LDS [NL][M] (log2 domain), each item's two (adjacent) rows read one
+// group before its stage A; inv.v[l]: 1 / the weight scale of layer l.
+#ifdef ECNF_SPLIT_WLDS
+__shared__ unsigned g_wlds_exp[8 * kPieces * 256];
+#endif
 template <int NF, int NL>
 __device__ __forceinline__ void chain_split(SplitX<NF>& XA, SplitX<NF>& XB, f32x16 (&acc)[NF],
                                             const unsigned* __restrict__ Wpk, const float* __restrict__ bias,
                                             const ChainInv& inv, int lane) {
-  using Plan = SplitPlan<NF>;
-  constexpr int GB = Plan::GB, GL = Plan::GL, G = NL * GL, M = NF * 32, PF = ECNF_SPLIT_PF;
-  constexpr int kMaxPair = 8;
+  using Plan = SplitPlan<NF, NL>;
+  constexpr int GB = Plan::GB, GL = Plan::GL, G = Plan::G, NI = Plan::NI, PF = ECNF_SPLIT_PF;
+  constexpr int GE = Plan::last_group() + 1;   // groups including the VALU-only tail
   const int kk = lane >> 5;
+  const float* lbias = bias + 4 * kk;
   const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned*>(Wpk), (short)0,
                                                                          0x7fffffff, 0x00020000);
   const int voff = lane * 16;
-  // task of global group gg (any layer), and the LDS bias address of its pair i
-  auto task_of = [](int gg2) constexpr { return Plan::task(gg2 % GL, gg2 / GL > 0); };
-  auto bias_row = [](int gg2, int i) constexpr {
-    const typename Plan::Task t = Plan::task(gg2 % GL, gg2 / GL > 0);
-    const int r = 2 * (t.p0 + i);
-    return (gg2 / GL + t.dl) * M + t.j * 32 + 8 * (r >> 2) + (r & 3);
-  };
   u32x4 wbuf[PF + 1][kPieces];
 #pragma unroll
   for (int gg = 0; gg < PF && gg < G; ++gg)
 #pragma unroll
     for (int p = 0; p < kPieces; ++p) wbuf[gg][p] = wload(rsrc, voff, (gg * kPieces + p) * kPieceBytes);
-  f32x2 bcur[kMaxPair], bnext[kMaxPair];
-  f32x2 ybuf[2][kMaxPair];                                // stage-1 results, by group parity
-  {
-    constexpr typename Plan::Task t0 = Plan::task(0, false);
-    if constexpr (t0.j >= 0)
-      static_for<t0.p1 - t0.p0>([&](auto Ic) {
-        bcur[Ic] = *reinterpret_cast<const f32x2*>(bias + bias_row(0, Ic) + 4 * kk);
-      });
-  }
-  static_for<G>([&](auto GGc) {
+  // per-item pipeline registers (SSA after unrolling: only live items occupy registers)
+  f32x2 bv[NI], uv[NI], ev[NI];
+  static_for<Plan::count(0, 0)>([&](auto Kc) {
+    constexpr int id = Plan::nth(0, 0, decltype(Kc)::value);
+    bv[id] = *reinterpret_cast<const f32x2*>(lbias + Plan::bias_off(id));
+  });
+  static_for<GE>([&](auto GGc) {
     constexpr int gg = decltype(GGc)::value;
+    constexpr bool mfma_group = gg < G;
     constexpr int l = gg / GL, g = gg % GL, jb = g / GB, fb = (g % GB) >> 1, u = g & 1;
-    constexpr typename Plan::Task tk = task_of(gg);
-    constexpr int tl = l + tk.dl;                          // layer whose block is activated here
-    constexpr bool split_out = tl < NL - 1;                // final layer stays fp32 in acc
-    constexpr int npair = tk.j >= 0 ? tk.p1 - tk.p0 : 0;
-    auto& Xin = pick<l & 1>(XA, XB);
+    constexpr int nA = Plan::count(gg, 0), nB = Plan::count(gg, 1), nC = Plan::count(gg, 2);
+    constexpr int nbias = Plan::count(gg + 1, 0);
+#if defined(ECNF_SPLIT_WLDS)   // timing experiment: fragments from an LDS image of 8 groups (g_wlds_exp)
+    if constexpr (gg + PF < G) {
+#pragma unroll
+      for (int p = 0; p < kPieces; ++p)
+        wbuf[(gg + PF) % (PF + 1)][p] =
+            *reinterpret_cast<const u32x4*>(g_wlds_exp + ((((gg + PF) & 7) * kPieces + p) * 256 + lane * 4));
+    }
+#elif !defined(ECNF_SPLIT_NO_WLOAD)   // NO_WLOAD timing experiment: reuse the first PF groups' weights
     if constexpr (gg + PF < G) {
 #pragma unroll
       for (int p = 0; p < kPieces; ++p)
         wbuf[(gg + PF) % (PF + 1)][p] = wload(rsrc, voff, ((gg + PF) * kPieces + p) * kPieceBytes);
     }
-    // biases of the next group's pairs
-    constexpr int nnext = (gg + 1 < G && task_of(gg + 1).j >= 0) ? task_of(gg + 1).p1 - task_of(gg + 1).p0 : 0;
-    static_for<nnext>([&](auto Ic) {
-      bnext[Ic] = *reinterpret_cast<const f32x2*>(bias + bias_row(gg + 1, Ic) + 4 * kk);
-    });
-    const u32x4* A = wbuf[gg % (PF + 1)];
-    const u32x4* B = Xin.v[fb][u];
-    static_for<kTerms>([&](auto Tc) {
-      constexpr int t = decltype(Tc)::value;
-      constexpr int pa = term_w(t), pb = term_x(t);   // cross terms, smallest first
-      if constexpr (fb == 0 && u == 0 && t == 0) {
-        const f32x16 z = {};
-        acc[jb] = mfma_split(A[pa], B[pb], z);
-      } else {
-        acc[jb] = mfma_split(A[pa], B[pb], acc[jb]);
-      }
-    });
-#ifndef ECNF_SPLIT_NO_ACT
-    // stage 2 of the previous group's pairs (split into that layer's output buffer)
-    if constexpr (gg > 0) {
-      constexpr typename Plan::Task tp = task_of(gg - 1);
-      constexpr int lp = (gg - 1) / GL + tp.dl;
-      if constexpr (tp.j >= 0 && lp < NL - 1) {
-        auto& Xp = pick<(lp + 1) & 1>(XA, XB);
-        static_for<tp.p1 - tp.p0>([&](auto Ic) {
-          constexpr int i = decltype(Ic)::value;
-          put_pair<NF, tp.j, 2 * (tp.p0 + i)>(Xp, ybuf[(gg - 1) & 1][i][0], ybuf[(gg - 1) & 1][i][1]);
-        });
-      }
-    }
-    // stage 1 of this group's pairs
-    static_for<npair>([&](auto Ic) {
-      constexpr int i = decltype(Ic)::value;
-      ybuf[gg & 1][i] = act_stage1<NF, (tk.j < 0 ? 0 : tk.j), 2 * (tk.p0 + i), split_out>(acc, bcur[i], inv.v[tl]);
-    });
 #endif
-    // schedule: weight loads, bias reads, then MFMA / VALU alternating
-    constexpr int nvalu = npair * 16 + (kPieces == 3 ? 12 : 1) *
-                                            ((gg > 0 && task_of(gg - 1).j >= 0) ? task_of(gg - 1).p1 - task_of(gg - 1).p0 : 0);
-    constexpr int per = (nvalu + kTerms - 1) / kTerms;
-#ifndef ECNF_SPLIT_NO_SGB
-    if constexpr (gg + PF < G) __builtin_amdgcn_sched_group_barrier(0x020, kPieces, 0);
-    if constexpr (nnext > 0) __builtin_amdgcn_sched_group_barrier(0x100, nnext, 0);
-    static_for<kTerms>([&](auto) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      if constexpr (per > 0) __builtin_amdgcn_sched_group_barrier(0x002, per, 0);
+    // biases of the next group's stage-A items
+    static_for<nbias>([&](auto Kc) {
+      constexpr int id = Plan::nth(gg + 1, 0, decltype(Kc)::value);
+      bv[id] = *reinterpret_cast<const f32x2*>(lbias + Plan::bias_off(id));
     });
-#endif
-    __builtin_amdgcn_sched_barrier(0);
-    static_for<nnext>([&](auto Ic) { bcur[Ic] = bnext[Ic]; });
-  });
-  {
-    constexpr typename Plan::Task tp = task_of(G - 1);
-    constexpr int lp = (G - 1) / GL + tp.dl;
-    if constexpr (tp.j >= 0 && lp < NL - 1) {
-      auto& Xp = pick<(lp + 1) & 1>(XA, XB);
-      static_for<tp.p1 - tp.p0>([&](auto Ic) {
-        constexpr int i = decltype(Ic)::value;
-        put_pair<NF, tp.j, 2 * (tp.p0 + i)>(Xp, ybuf[(G - 1) & 1][i][0], ybuf[(G - 1) & 1][i][1]);
+    if constexpr (mfma_group) {
+      auto& Xin = pick<l & 1>(XA, XB);
+      const u32x4* A = wbuf[gg % (PF + 1)];
+      const u32x4* B = Xin.v[fb][u];
+      static_for<kTerms>([&](auto Tc) {
+        constexpr int t = decltype(Tc)::value;
+        constexpr int pa = term_w(t), pb = term_x(t);   // cross terms, smallest first
+        if constexpr (fb == 0 && u == 0 && t == 0) {
+          const f32x16 z = {};
+          acc[jb] = mfma_split(A[pa], B[pb], z);
+        } else {
+          acc[jb] = mfma_split(A[pa], B[pb], acc[jb]);
+        }
       });
     }
-  }
-  // the final layer's last block
-  static_for<8>([&](auto Ic) {
-    constexpr int i = decltype(Ic)::value;
-    const f32x2 b2 = *reinterpret_cast<const f32x2*>(bias + (NL - 1) * M + (NF - 1) * 32 + 8 * ((2 * i) >> 2) +
-                                                     ((2 * i) & 3) + 4 * kk);
-    act_pair<NF, NF - 1, 2 * i, false>(acc, XA, b2, inv.v[NL - 1]);
+#if defined(ECNF_SPLIT_CHEAP_ACT)   // timing experiment: keep the data flow (one VALU per pair), drop the arithmetic
+    static_for<nC>([&](auto Kc) {
+      constexpr int id = Plan::nth(gg, 2, decltype(Kc)::value);
+      constexpr typename Plan::Item it = Plan::item(id);
+      constexpr int r = 2 * it.p;
+      if constexpr (it.l < NL - 1) {
+        auto& Xo = pick<(it.l + 1) & 1>(XA, XB);
+        Xo.v[it.j][r >> 3][0][(r & 7) >> 1] =
+            __builtin_bit_cast(unsigned, acc[it.j][r]) ^ __builtin_bit_cast(unsigned, acc[it.j][r + 1]);
+      }
+    });
+#elif !defined(ECNF_SPLIT_NO_ACT)
+    // stage A
+    static_for<nA>([&](auto Kc) {
+      constexpr int id = Plan::nth(gg, 0, decltype(Kc)::value);
+      constexpr typename Plan::Item it = Plan::item(id);
+      constexpr int r = 2 * it.p;
+      uv[id][0] = fmaf(acc[it.j][r], inv.v[it.l], bv[id][0]);
+      uv[id][1] = fmaf(acc[it.j][r + 1], inv.v[it.l], bv[id][1]);
+      ev[id][0] = __builtin_amdgcn_exp2f(uv[id][0]);
+      ev[id][1] = __builtin_amdgcn_exp2f(uv[id][1]);
+    });
+    // stage B
+    static_for<nB>([&](auto Kc) {
+      constexpr int id = Plan::nth(gg, 1, decltype(Kc)::value);
+      ev[id][0] = __builtin_amdgcn_rcpf(1.0f + ev[id][0]);
+      ev[id][1] = __builtin_amdgcn_rcpf(1.0f + ev[id][1]);
+    });
+    // stage C
+    static_for<nC>([&](auto Kc) {
+      constexpr int id = Plan::nth(gg, 2, decltype(Kc)::value);
+      constexpr typename Plan::Item it = Plan::item(id);
+      const float y0 = uv[id][0] * ev[id][0];
+      const float y1 = uv[id][1] * ev[id][1];
+      if constexpr (it.l < NL - 1) {
+        put_pair<NF, it.j, 2 * it.p>(pick<(it.l + 1) & 1>(XA, XB), y0, y1);
+      } else {
+        acc[it.j][2 * it.p] = y0;
+        acc[it.j][2 * it.p + 1] = y1;
+      }
+    });
+#endif
+    if constexpr (mfma_group) {
+      // schedule: weight loads, bias reads, then MFMA / VALU alternating
+      constexpr int nvalu = 4 * nA + 4 * nB + 3 * nC;
+      constexpr int per = (nvalu + kTerms - 1) / kTerms;
+#ifndef ECNF_SPLIT_NO_SGB
+#if defined(ECNF_SPLIT_WLDS)
+      if constexpr (gg + PF < G) __builtin_amdgcn_sched_group_barrier(0x100, kPieces, 0);
+#elif !defined(ECNF_SPLIT_NO_WLOAD)
+      if constexpr (gg + PF < G) __builtin_amdgcn_sched_group_barrier(0x020, kPieces, 0);
+#endif
+      if constexpr (nbias > 0) __builtin_amdgcn_sched_group_barrier(0x100, nbias, 0);
+      static_for<kTerms>([&](auto) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        if constexpr (per > 0) __builtin_amdgcn_sched_group_barrier(0x002, per, 0);
+      });
+#endif
+      __builtin_amdgcn_sched_barrier(0);
+    }
   });
 }

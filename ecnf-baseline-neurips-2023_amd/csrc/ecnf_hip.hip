@@ -803,6 +803,7 @@ int ecnf_create(const ecnf_cfg* cfg, const float* params, size_t n_floats, int d
   Packer pk;
   struct Off {
     size_t Wn, bn, Wp, bp, wd, We, Ws, be, wx, wg, Wh[kMaxPhiH], bh[kMaxPhiH], Wn_s, Wp_s, Wh_s[kMaxPhiH];
+    size_t bp_u, wd_u, be_u, wg_u, wx_u;
     float bx, bg;
     float cinv[2 * 4 - 1], ninv, pinv, hinv[kMaxPhiH];
   };
@@ -829,7 +830,17 @@ int ecnf_create(const ecnf_cfg* cfg, const float* params, size_t n_floats, int d
     for (int j = 0; j < M; ++j) { bp[M + j] = b.eb[0][j]; wd[j] = b.ek[0][(size_t)2 * H * M + j]; }
     o.Wp = pk.put(wp.data(), wp.size());
     o.Wn_s = put_split_node(b.nk, H + T, H, &o.ninv);
-    o.Wp_s = put_split_node(wp.data(), H, 2 * M, &o.pinv);
+    // log2-domain copies for the split kernels (chain_split.hpp, silu_u)
+    constexpr float kNegLog2e = -1.4426950408889634f, kNegLn2 = -0.69314718055994531f;
+    auto scaled = [](const float* v, size_t n, float f) {
+      std::vector<float> r(v, v + n);
+      for (auto& x : r) x *= f;
+      return r;
+    };
+    const std::vector<float> wp_u = scaled(wp.data(), wp.size(), kNegLog2e);
+    o.Wp_s = put_split_node(wp_u.data(), H, 2 * M, &o.pinv);
+    o.bp_u = pk.put(scaled(bp.data(), bp.size(), kNegLog2e).data(), bp.size());
+    o.wd_u = pk.put(scaled(wd.data(), wd.size(), kNegLog2e).data(), wd.size());
     o.bp = pk.put(bp.data(), bp.size());
     o.wd = pk.put(wd.data(), wd.size());
     // chain: phi_e.1..L-1, phi_x.0..L-1, each [M][M] -> fragment order
@@ -863,8 +874,11 @@ int ecnf_create(const ecnf_cfg* cfg, const float* params, size_t n_floats, int d
     }
     o.Ws = pk.put(reinterpret_cast<const float*>(ws.data()), ws.size());
     o.be = pk.put(be.data(), be.size());
+    o.be_u = pk.put(scaled(be.data(), be.size(), kNegLog2e).data(), be.size());
     o.wx = pk.put(b.xk, M);
     o.wg = pk.put(b.gk, M);
+    o.wx_u = pk.put(scaled(b.xk, M, kNegLn2).data(), M);
+    o.wg_u = pk.put(scaled(b.gk, M, kNegLn2).data(), M);
     o.bx = *b.xb;
     o.bg = *b.gb;
     for (int l = 0; l <= L; ++l) {
@@ -914,6 +928,8 @@ int ecnf_create(const ecnf_cfg* cfg, const float* params, size_t n_floats, int d
         w.Wh_s[l] = reinterpret_cast<const unsigned*>(dbuf + o.Wh_s[l]);
       }
       w.Wn_s = reinterpret_cast<const unsigned*>(dbuf + o.Wn_s);
+      w.bp_u = dbuf + o.bp_u; w.wd_u = dbuf + o.wd_u; w.be_u = dbuf + o.be_u; w.wg_u = dbuf + o.wg_u;
+      w.wx_u = dbuf + o.wx_u;
       for (int cl = 0; cl < 2 * 4 - 1; ++cl) w.cinv[cl] = o.cinv[cl];
       w.ninv = o.ninv;
       w.pinv = o.pinv;

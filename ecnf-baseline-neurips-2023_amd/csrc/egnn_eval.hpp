@@ -84,6 +84,9 @@ struct BlockW {
   const float* Wh[kMaxPhiH]; const float* bh[kMaxPhiH];  // phi_h layers, row-major [in][out]
   // split node GEMM fragments [out block][16-deep k-step][piece][lane] (node_task_split)
   const unsigned* Wn_s; const unsigned* Wp_s; const unsigned* Wh_s[kMaxPhiH];
+  // log2-domain copies for the split kernels (chain_split.hpp, silu_u): -log2(e) x {phi_e.0 Wp (in Wp_s), bp, w_d,
+  // chain biases}, -ln 2 x {w_g, w_x}
+  const float* bp_u; const float* wd_u; const float* be_u; const float* wg_u; const float* wx_u;
   // 1 / the power-of-two scale of each split weight matrix (chain_split.hpp): chain layers, Wn, Wp, phi_h
   float cinv[2 * 4 - 1];
   float ninv, pinv, hinv[kMaxPhiH];
@@ -828,9 +831,9 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
         static_for<2>([&](auto Hc) {
           constexpr int e = 2 * decltype(Hc)::value;
           const int row = fb * 32 + 8 * q + 4 * kk + e;
-          const float p0 = Ps[row] + Pr[row] + len2 * w[e];
-          const float p1 = Ps[row + 1] + Pr[row + 1] + len2 * w[e + 1];
-          put_pair<NF, fb, 4 * q + e>(XA, p0 * sigmoidf_(p0), p1 * sigmoidf_(p1));
+          const float u0 = Ps[row] + Pr[row] + len2 * w[e];   // log2 domain (silu_u)
+          const float u1 = Ps[row + 1] + Pr[row + 1] + len2 * w[e + 1];
+          put_pair<NF, fb, 4 * q + e>(XA, silu_u(u0), silu_u(u1));
         });
       });
     });
@@ -855,7 +858,7 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
                                   put_pair<NF, fb, 2 * i>(XA, m[fb][2 * i], m[fb][2 * i + 1]);
                                 });
                               });
-                              const unsigned* Wx = launder_uniform(bw.Ws + (size_t)(L - 1) * SplitPlan<NF>::GL * kGroupU32);
+                              const unsigned* Wx = launder_uniform(bw.Ws + (size_t)(L - 1) * SplitPlan<NF, 1>::GL * kGroupU32);
                               chain_split<NF, L>(XA, XB, m, Wx, s.vecs + (L - 1) * NF * 32, ix, lane);
                             });
     STAMP_LANE0(s, kStEdgeTail, t_sub);
@@ -960,14 +963,20 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
   for (int k = 0; k < net.K; ++k) {
     const BlockW& bw = net.blk[k];
     // stage this block's chain biases and the w_d / w_g / w_x vectors in LDS (read by every edge tile)
-    for (int idx = tid; idx < (2 * L + 2) * M; idx += kNT) {
-      const int v = idx / M, c = idx - v * M;
-      float val;
-      if (v < 2 * L - 1) val = gptr(bw.be)[idx];
-      else if (v == 2 * L - 1) val = gptr(bw.wd)[c];
-      else if (v == 2 * L) val = gptr(bw.wg)[c];
-      else val = gptr(bw.wx)[c];
-      s.vecs[idx] = val;
+    {
+      const float* be = kSplitG ? bw.be_u : bw.be;
+      const float* wd = kSplitG ? bw.wd_u : bw.wd;
+      const float* wg = kSplitG ? bw.wg_u : bw.wg;
+      const float* wx = kSplitG ? bw.wx_u : bw.wx;
+      for (int idx = tid; idx < (2 * L + 2) * M; idx += kNT) {
+        const int v = idx / M, c = idx - v * M;
+        float val;
+        if (v < 2 * L - 1) val = gptr(be)[idx];
+        else if (v == 2 * L - 1) val = gptr(wd)[c];
+        else if (v == 2 * L) val = gptr(wg)[c];
+        else val = gptr(wx)[c];
+        s.vecs[idx] = val;
+      }
     }
     // h <- Dense([h | temb])  (egnn.py:166-167)
     node_gemm<NT, kNW, kSplitG>(s.hin, s.ld_hin, H + T, nullptr, 0, 0, bw.Wn, bw.Wn_s, bw.ninv, H, bw.bn, H, false, nullptr, 0, s.hb, s.ld_hb, RP,
@@ -975,7 +984,7 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
     __syncthreads();
     STAMP(s, kStNodeDense);
     // per-node halves of phi_e layer 1
-    node_gemm<NT, kNW, kSplitG>(s.hb, s.ld_hb, H, nullptr, 0, 0, bw.Wp, bw.Wp_s, bw.pinv, 2 * M, bw.bp, 2 * M, false, nullptr, 0, s.P, s.ld_P, RP,
+    node_gemm<NT, kNW, kSplitG>(s.hb, s.ld_hb, H, nullptr, 0, 0, bw.Wp, bw.Wp_s, bw.pinv, 2 * M, kSplitG ? bw.bp_u : bw.bp, 2 * M, false, nullptr, 0, s.P, s.ld_P, RP,
                   nvalid, wave, lane);
     __syncthreads();
     STAMP(s, kStPGemm);
@@ -997,7 +1006,9 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
     }
     for (int idx = tid; idx < R * M; idx += kNT) {
       const int row = idx / M, c = idx - row * M;
-      s.macc[row * s.ld_m + c] /= net.sqrt_nn1;
+      float mv = s.macc[row * s.ld_m + c];
+      if constexpr (kSplitG) mv *= -0.69314718055994531f;   // log2-domain messages (chain_split.hpp, silu_u)
+      s.macc[row * s.ld_m + c] = mv / net.sqrt_nn1;
     }
     __syncthreads();
     STAMP(s, kStNodeUpd);

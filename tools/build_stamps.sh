@@ -2,6 +2,6 @@
 # Diagnostic build with in-kernel phase stamps (never the product library).
 set -e
 ROOT="$(cd "$(dirname "$0")/.." && pwd)"
-/opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -std=c++17 -fPIC -shared -Wno-pass-failed -Wno-unused-value \
+/opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -std=c++17 -fPIC -shared -fno-slp-vectorize -mllvm -amdgpu-mfma-vgpr-form -Wno-pass-failed -Wno-unused-value \
   -Wno-unused-result -DECNF_STAMPS -I "$ROOT/include" -o "$ROOT/tools/libecnf_hip_stamps.so" \
   "$ROOT/ecnf-baseline-neurips-2023_amd/csrc/ecnf_hip.hip"

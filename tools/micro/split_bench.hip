@@ -7,13 +7,18 @@ using namespace ecnf;
 #ifndef TILES
 #define TILES 16
 #endif
+#ifndef WAVES   // waves per workgroup (= per CU: the launch reserves 120 KiB of LDS per workgroup)
+#define WAVES 4
+#endif
 constexpr int NF = 4, M = 128;
 constexpr size_t kLayerU32 = (size_t)2 * NF * NF * kGroupU32;
 
-__global__ __launch_bounds__(256) void kern(const unsigned* __restrict__ W, const float* __restrict__ b, float* out,
+__global__ __launch_bounds__(64 * WAVES) void kern(const unsigned* __restrict__ W, const float* __restrict__ b, float* out,
                                             unsigned long long* cyc) {
   __shared__ float bias[5 * M];
-  for (int i = threadIdx.x; i < 5 * M; i += 256) bias[i] = b[i];
+  for (int i = threadIdx.x; i < 5 * M; i += 64 * WAVES) bias[i] = b[i];
+  extern __shared__ float pad[];
+  if (threadIdx.x == 0) pad[0] = 0.f;
   __syncthreads();
   const int lane = threadIdx.x & 63;
   SplitX<NF> XA, XB;
@@ -46,8 +51,8 @@ __global__ __launch_bounds__(256) void kern(const unsigned* __restrict__ W, cons
   float s = 0.f;
   for (int f = 0; f < NF; ++f)
     for (int r = 0; r < 16; ++r) s += acc[f][r];
-  out[blockIdx.x * 256 + threadIdx.x] = s;
-  if (lane == 0) cyc[blockIdx.x * 4 + (threadIdx.x >> 6)] = t1 - t0;
+  out[blockIdx.x * 64 * WAVES + threadIdx.x] = s;
+  if (lane == 0) cyc[blockIdx.x * WAVES + (threadIdx.x >> 6)] = t1 - t0;
 }
 
 int main() {
@@ -61,14 +66,15 @@ int main() {
   (void)hipMalloc(&cyc, 256 * 4 * 8);
   (void)hipMemcpy(W, hw.data(), nW * 4, hipMemcpyHostToDevice);
   (void)hipMemcpy(b, hb.data(), 5 * M * 4, hipMemcpyHostToDevice);
-  std::vector<unsigned long long> hc(256 * 4);
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 120 * 1024);
+  std::vector<unsigned long long> hc(256 * WAVES);
   for (int rep = 0; rep < 4; ++rep) {
     hipEvent_t e0, e1; (void)hipEventCreate(&e0); (void)hipEventCreate(&e1);
     (void)hipEventRecord(e0);
-    hipLaunchKernelGGL(kern, dim3(256), dim3(256), 0, 0, W, b, out, cyc);
+    hipLaunchKernelGGL(kern, dim3(256), dim3(64 * WAVES), 120 * 1024, 0, W, b, out, cyc);
     (void)hipEventRecord(e1); (void)hipEventSynchronize(e1);
     float ms; (void)hipEventElapsedTime(&ms, e0, e1);
-    (void)hipMemcpy(hc.data(), cyc, 256 * 4 * 8, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(hc.data(), cyc, 256 * WAVES * 8, hipMemcpyDeviceToHost);
     double m = 0; for (auto c : hc) m += c; m /= hc.size();
     if (rep == 3) printf("split chain: %.0f cycles/layer (MFMA-bound %d), %.3f ms\n", m / (TILES * 5.0), 32 * kTerms * 32, ms);
   }
