@@ -1,0 +1,453 @@
+// ecnf_kernels.hpp — the device side of libecnf_hip.so: the ODE integrator and vector-field kernels and their
+// templated launchers (included by ecnf_hip.hip, which either instantiates every compiled shape itself or, in
+// the split build, declares them extern; and by ecnf_part.hip, one translation unit per compiled shape).
+//
+//   vf_kernel        one EGNN evaluation (+ JVPs) per molecule      <- cnf.apply / jax.vjp
+//   integrate_kernel the whole ODE solve, one launch: each workgroup integrates its MPW molecules end to end
+//                    (Euler / Dopri5 fixed step / Dopri5 + PID per molecule), state in LDS, the EGNN eval
+//                    as a device function                            <- diffrax.diffeqsolve
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/ecnf.h"
+#include "egnn_eval.hpp"
+
+namespace ecnf {
+
+// ---------------------------------------------------------------------------------------------------
+// Dopri5 tableau (diffrax 2023: Shampine's embedded pair, FSAL)
+// ---------------------------------------------------------------------------------------------------
+__constant__ float kA[6][6] = {
+    {(float)(1.0 / 5), 0, 0, 0, 0, 0},
+    {(float)(3.0 / 40), (float)(9.0 / 40), 0, 0, 0, 0},
+    {(float)(44.0 / 45), (float)(-56.0 / 15), (float)(32.0 / 9), 0, 0, 0},
+    {(float)(19372.0 / 6561), (float)(-25360.0 / 2187), (float)(64448.0 / 6561), (float)(-212.0 / 729), 0, 0},
+    {(float)(9017.0 / 3168), (float)(-355.0 / 33), (float)(46732.0 / 5247), (float)(49.0 / 176),
+     (float)(-5103.0 / 18656), 0},
+    {(float)(35.0 / 384), 0.0f, (float)(500.0 / 1113), (float)(125.0 / 192), (float)(-2187.0 / 6784),
+     (float)(11.0 / 84)}};
+__constant__ float kC[7] = {0.0f, (float)(1.0 / 5), (float)(3.0 / 10), (float)(4.0 / 5), (float)(8.0 / 9), 1.0f, 1.0f};
+__constant__ float kBerr[7] = {(float)(35.0 / 384 - 1951.0 / 21600),
+                               0.0f,
+                               (float)(500.0 / 1113 - 22642.0 / 50085),
+                               (float)(125.0 / 192 - 451.0 / 720),
+                               (float)(-2187.0 / 6784 + 12231.0 / 42400),
+                               (float)(11.0 / 84 - 649.0 / 6300),
+                               (float)(-1.0 / 60.0)};
+
+struct SolveP {
+  int solver, div, adaptive, max_steps;
+  float tau0, tau1, dirf, dt0, rtol, atol, dtmin;
+};
+
+// solver state in LDS, after the eval region
+struct SolverLds {
+  float *ys, *vout, *tin, *tout, *y, *eps, *kx;   // [MPW][ND] each, kx [7][MPW][ND]
+  float *ts, *divv, *lp, *kl, *tau, *tnext, *dt, *h, *l1, *h0;   // [MPW] (kl: [7][MPW])
+  int *active, *atmin, *nfe, *steps, *status, *keep, *any;
+};
+
+__host__ __device__ inline int solver_lds_floats(int MPW, int ND) {
+  return 13 * align4(MPW * ND) + 16 * align4(MPW) + 8 * align4(MPW) + 4;
+}
+
+__device__ inline SolverLds carve_solver(float* p, int MPW, int ND) {
+  SolverLds st;
+  const int a = align4(MPW * ND), b = align4(MPW);
+  st.ys = p; p += a;  st.vout = p; p += a;  st.tin = p; p += a;  st.tout = p; p += a;
+  st.y = p; p += a;   st.eps = p; p += a;   st.kx = p; p += 7 * a;
+  st.ts = p; p += b;  st.divv = p; p += b;  st.lp = p; p += b;   st.kl = p; p += 7 * b;
+  st.tau = p; p += b; st.tnext = p; p += b; st.dt = p; p += b;   st.h = p; p += b;
+  st.l1 = p; p += b;  st.h0 = p; p += b;
+  int* q = reinterpret_cast<int*>(p);
+  st.active = q; q += b; st.atmin = q; q += b; st.nfe = q; q += b; st.steps = q; q += b;
+  st.status = q; q += b; st.keep = q; q += b; st.any = q;
+  return st;
+}
+
+__device__ inline float clip_end(float tn, float tau1) { return tn > tau1 - 1e-6f ? tau1 : tn; }
+
+// one evaluation of the joint field g(tau, y) = dir * f(dir * tau, y) at (st.ts, st.ys) for every molecule
+// of the workgroup; writes kx_out [MPW][ND] and kl_out [MPW].  Exactly one egnn_eval call site (it is inlined).
+template <int NF, int NT, int L, int D>
+__device__ __forceinline__ void joint_field(const Net& net, const Lds& s, const SolverLds& st, const SolveP& sp,
+                                            float* kx_out, float* kl_out) {
+  constexpr int kThreads = Geo<NF, NT>::NTHR;
+  const int tid = threadIdx.x, MPW = net.MPW, ND = net.ND;
+  // NT == 0: one primal eval; Hutchinson: one JVP along eps; exact: ND JVPs along e_k (trace of J)
+  const int nrep = (NT == 0 || sp.div == ECNF_DIV_HUTCHINSON) ? 1 : ND;
+  if (tid < MPW) st.divv[tid] = 0.f;
+  for (int k = 0; k < nrep; ++k) {
+    if constexpr (NT) {
+      if (sp.div == ECNF_DIV_HUTCHINSON) {
+        for (int i = tid; i < MPW * ND; i += kThreads) st.tin[i] = st.eps[i];
+      } else {
+        for (int i = tid; i < MPW * ND; i += kThreads) st.tin[i] = ((i % ND) == k) ? 1.0f : 0.0f;
+      }
+      __syncthreads();
+    }
+    egnn_eval<NF, NT, L, D>(net, s, st.ys, st.ts, st.tin, st.vout, st.tout);
+    if constexpr (NT) {
+      if (tid < MPW) {
+        if (sp.div == ECNF_DIV_HUTCHINSON) {
+          float acc = 0.f;
+          for (int c = 0; c < ND; ++c) acc += st.tout[tid * ND + c] * st.eps[tid * ND + c];
+          st.divv[tid] = acc;
+        } else {
+          st.divv[tid] += st.tout[tid * ND + k];
+        }
+      }
+    }
+  }
+  for (int i = tid; i < MPW * ND; i += kThreads) kx_out[i] = sp.dirf * st.vout[i];
+  if (tid < MPW) {
+    kl_out[tid] = sp.dirf * st.divv[tid];
+    if (st.active[tid]) st.nfe[tid] += 1;
+  }
+  __syncthreads();
+}
+
+// diffrax rms_norm over the leaves of one molecule's state: (x, logp) when the divergence is tracked
+// (get_log_prob / sample_and_log_prob_cnf), x alone for sample_cnf (sample_and_log_prob.py:28-37 has y0 = x0)
+__device__ inline float rms_state(float sumsq_x, float l, int ND, bool track) {
+  return track ? sqrtf((sumsq_x + l * l) / (float)(ND + 1)) : sqrtf(sumsq_x / (float)ND);
+}
+
+enum Phase { kEuler = 0, kInit0 = 1, kInit1 = 2, kFsal = 3, kStage = 4 };
+
+// The whole solve as a phase machine around ONE field evaluation per loop trip.
+template <int NF, int NT, int L, int D>
+__global__ __launch_bounds__((Geo<NF, NT>::NTHR)) void integrate_kernel(Net net, SolveP sp, const float* __restrict__ y0,
+                                                                  const int32_t* __restrict__ feat,
+                                                                  const float* __restrict__ eps, float* y1,
+                                                                  float* dlogp, int32_t* nfe_out,
+                                                                  int32_t* status_out, int B) {
+  constexpr int kThreads = Geo<NF, NT>::NTHR;
+  extern __shared__ float smem[];
+  const int tid = threadIdx.x, MPW = net.MPW, ND = net.ND, N = net.N;
+  const Lds s = carve_lds<NT>(net, smem);
+  const SolverLds st = carve_solver(s.tail, MPW, ND);
+  const int mol0 = blockIdx.x * MPW;
+  const int nmol = min(MPW, B - mol0);
+  const int a = align4(MPW * ND), b = align4(MPW);
+  const bool track = sp.div != ECNF_DIV_NONE;
+
+  // zero the eval scratch (aggregates must start at +0; padding rows stay finite)
+  for (int i = tid; i < (int)(s.tail - smem); i += kThreads) smem[i] = 0.f;
+  __syncthreads();
+  for (int i = tid; i < MPW * ND; i += kThreads) {
+    const int m = i / ND;
+    st.y[i] = m < nmol ? y0[(size_t)mol0 * ND + i] : 0.f;
+    st.eps[i] = (m < nmol && eps) ? eps[(size_t)mol0 * ND + i] : 0.f;
+  }
+  for (int i = tid; i < MPW * N; i += kThreads) s.feat[i] = (i / N) < nmol ? feat[(size_t)mol0 * N + i] : 0;
+  if (tid < MPW) {
+    st.lp[tid] = 0.f;
+    st.tau[tid] = sp.tau0;
+    st.active[tid] = tid < nmol ? 1 : 0;
+    st.atmin[tid] = 0;
+    st.nfe[tid] = 0;
+    st.steps[tid] = 0;
+    st.status[tid] = ECNF_OK;
+    st.dt[tid] = sp.dt0;
+    st.tnext[tid] = clip_end(fminf(sp.tau0 + sp.dt0, sp.tau1), sp.tau1);
+  }
+  __syncthreads();
+
+  // Euler: ConstantStepSize, all molecules share the (uniform, register-held) time grid
+  float e_tau = sp.tau0, e_tn = clip_end(sp.tau0 + sp.dt0, sp.tau1), e_h = 0.f;
+  int e_steps = 0;
+  int phase = sp.solver == ECNF_SOLVER_EULER ? kEuler : (sp.adaptive ? kInit0 : kFsal);
+  int stage = 1;
+
+#ifdef ECNF_STAMPS
+  if (tid == 0) {
+    for (int i = 0; i < 32; ++i) s.stamps[i] = 0;
+    s.stamps[31] = __builtin_amdgcn_s_memtime();
+    s.stamps[30] = __builtin_amdgcn_s_memrealtime();
+  }
+#endif
+  while (true) {
+    STAMP(s, kStSolver);
+    // ------------------------------------------------ inputs of this evaluation
+    float* kx_out;
+    float* kl_out;
+    if (phase == kEuler) {
+      if (!(e_tau < sp.tau1)) break;
+      if (++e_steps > sp.max_steps) {
+        if (tid < nmol) st.status[tid] = ECNF_E_MAX_STEPS;
+        break;
+      }
+      e_h = e_tn - e_tau;
+      for (int i = tid; i < MPW * ND; i += kThreads) st.ys[i] = st.y[i];
+      if (tid < MPW) st.ts[tid] = sp.dirf * e_tau;
+      kx_out = st.kx; kl_out = st.kl;
+    } else if (phase == kInit0 || phase == kFsal) {
+      for (int i = tid; i < MPW * ND; i += kThreads) st.ys[i] = st.y[i];
+      if (tid < MPW) st.ts[tid] = sp.dirf * st.tau[tid];
+      kx_out = st.kx; kl_out = st.kl;
+    } else if (phase == kInit1) {
+      for (int i = tid; i < MPW * ND; i += kThreads) st.ys[i] = st.y[i] + st.h0[i / ND] * st.kx[i];
+      if (tid < MPW) st.ts[tid] = sp.dirf * (st.tau[tid] + st.h0[tid]);
+      kx_out = st.kx + a; kl_out = st.kl + b;
+    } else {
+      if (stage == 1) {
+        if (tid == 0) {
+          int any = 0;
+          for (int m = 0; m < MPW; ++m) any |= st.active[m];
+          *st.any = any;
+        }
+        if (tid < MPW) st.h[tid] = st.tnext[tid] - st.tau[tid];
+        __syncthreads();
+        if (*st.any == 0) break;
+      }
+      for (int i = tid; i < MPW * ND; i += kThreads) {
+        float acc = 0.f;
+        for (int j = 0; j < stage; ++j) acc += kA[stage - 1][j] * st.kx[j * a + i];
+        st.ys[i] = st.y[i] + st.h[i / ND] * acc;
+      }
+      if (tid < MPW) st.ts[tid] = sp.dirf * (st.tau[tid] + kC[stage] * st.h[tid]);
+      kx_out = st.kx + stage * a; kl_out = st.kl + stage * b;
+    }
+    __syncthreads();
+
+    joint_field<NF, NT, L, D>(net, s, st, sp, kx_out, kl_out);
+
+    // ------------------------------------------------ consume it
+    if (phase == kEuler) {
+      for (int i = tid; i < MPW * ND; i += kThreads) st.y[i] = st.y[i] + e_h * st.kx[i];
+      if (tid < MPW) st.lp[tid] = st.lp[tid] + e_h * st.kl[tid];
+      e_tau = e_tn;
+      e_tn = clip_end(e_tau + sp.dt0, sp.tau1);
+    } else if (phase == kInit0) {
+      // Hairer's initial step, part 1 (diffrax _select_initial_step)
+      if (tid < MPW) {
+        float sy = 0.f, sf = 0.f;
+        for (int c = 0; c < ND; ++c) {
+          const float yy = st.y[tid * ND + c];
+          const float sc = sp.atol + fabsf(yy) * sp.rtol;
+          sy += (yy / sc) * (yy / sc);
+          sf += (st.kx[tid * ND + c] / sc) * (st.kx[tid * ND + c] / sc);
+        }
+        const float scl = sp.atol + fabsf(st.lp[tid]) * sp.rtol;
+        const float d0 = rms_state(sy, st.lp[tid] / scl, ND, track);
+        const float d1 = rms_state(sf, st.kl[tid] / scl, ND, track);
+        const bool cond = (d0 < 1e-5f) || (d1 < 1e-5f);
+        const float d1s = cond ? 1.0f : d1;
+        st.h0[tid] = cond ? 1e-6f : 0.01f * (d0 / d1s);
+        st.l1[tid] = d1;   // stash d1
+      }
+      phase = kInit1;
+    } else if (phase == kInit1) {
+      if (tid < MPW) {
+        float s2 = 0.f;
+        for (int c = 0; c < ND; ++c) {
+          const float sc = sp.atol + fabsf(st.y[tid * ND + c]) * sp.rtol;
+          const float df = (st.kx[a + tid * ND + c] - st.kx[tid * ND + c]) / sc;
+          s2 += df * df;
+        }
+        const float scl = sp.atol + fabsf(st.lp[tid]) * sp.rtol;
+        const float h0 = st.h0[tid];
+        const float d1 = st.l1[tid];
+        const float d2 = rms_state(s2, (st.kl[b + tid] - st.kl[tid]) / scl, ND, track) / h0;
+        const float maxd = fmaxf(d1, d2);
+        const float h1 = maxd <= 1e-15f ? fmaxf(1e-6f, h0 * 1e-3f) : powf(0.01f / maxd, 0.2f);
+        const float dt = fminf(100.0f * h0, h1);
+        st.atmin[tid] = dt <= sp.dtmin ? 1 : 0;
+        st.dt[tid] = fmaxf(dt, sp.dtmin);
+        st.tnext[tid] = clip_end(fminf(st.tau[tid] + st.dt[tid], sp.tau1), sp.tau1);
+      }
+      phase = kFsal;
+    } else if (phase == kFsal) {
+      phase = kStage;
+      stage = 1;
+    } else if (stage < 6) {
+      ++stage;
+    } else {
+      // st.ys holds y1 (the stage-7 input uses a_7 = b_sol): error estimate and step control per molecule
+      if (tid < MPW) {
+        const int m = tid;
+        const float h = st.h[m];
+        float accl = 0.f;
+        for (int j = 0; j < 6; ++j) accl += kA[5][j] * st.kl[j * b + m];
+        const float l1 = st.lp[m] + h * accl;
+        st.l1[m] = l1;
+        int keep = 1;
+        float new_dt = sp.dt0;
+        int new_atmin = 0;
+        if (sp.adaptive) {
+          float ssum = 0.f;
+          for (int c = 0; c < ND; ++c) {
+            float e = 0.f;
+            for (int j = 0; j < 7; ++j) e += kBerr[j] * st.kx[j * a + m * ND + c];
+            e = h * e;
+            const float sc = sp.atol + fmaxf(fabsf(st.y[m * ND + c]), fabsf(st.ys[m * ND + c])) * sp.rtol;
+            ssum += (e / sc) * (e / sc);
+          }
+          float el = 0.f;
+          for (int j = 0; j < 7; ++j) el += kBerr[j] * st.kl[j * b + m];
+          el = h * el;
+          const float scl = sp.atol + fmaxf(fabsf(st.lp[m]), fabsf(l1)) * sp.rtol;
+          const float err = rms_state(ssum, el / scl, ND, track);
+          keep = (err < 1.0f) || st.atmin[m];
+          const float inv = 1.0f / err;
+          float factor = 0.9f * powf(inv, 0.2f);
+          factor = fminf(fmaxf(factor, keep ? 1.0f : 0.2f), 10.0f);
+          if (isnan(factor)) factor = 1.0f;
+          new_dt = h * factor;
+          new_atmin = new_dt <= sp.dtmin ? 1 : 0;
+          new_dt = fmaxf(new_dt, sp.dtmin);
+        }
+        st.keep[m] = keep && st.active[m];
+        st.dt[m] = new_dt;
+        st.h0[m] = (float)new_atmin;
+      }
+      __syncthreads();
+      for (int i = tid; i < MPW * ND; i += kThreads) {
+        const int m = i / ND;
+        if (st.keep[m]) {
+          st.y[i] = st.ys[i];
+          st.kx[i] = st.kx[6 * a + i];
+        }
+      }
+      if (tid < MPW) {
+        const int m = tid;
+        if (st.active[m]) {
+          if (st.keep[m]) {
+            st.lp[m] = st.l1[m];
+            st.kl[m] = st.kl[6 * b + m];
+            st.tau[m] = st.tnext[m];
+          }
+          st.atmin[m] = (int)st.h0[m];
+          st.steps[m] += 1;
+          st.tnext[m] = sp.adaptive ? clip_end(fminf(st.tau[m] + st.dt[m], sp.tau1), sp.tau1)
+                                    : clip_end(st.tau[m] + sp.dt0, sp.tau1);
+          if (!(st.tau[m] < sp.tau1)) {
+            st.active[m] = 0;
+          } else if (st.steps[m] >= sp.max_steps) {
+            st.status[m] = ECNF_E_MAX_STEPS;
+            st.active[m] = 0;
+          }
+        }
+      }
+      stage = 1;
+    }
+    __syncthreads();
+  }
+  __syncthreads();
+#ifdef ECNF_STAMPS
+  if (tid == 0) {
+    STAMP(s, kStSolver);
+    s.stamps[29] = __builtin_amdgcn_s_memrealtime() - s.stamps[30];
+    for (int i = 0; i < kStCount; ++i) atomicAdd(&g_stamps[i], s.stamps[i]);
+    atomicAdd(&g_stamps[29], s.stamps[29]);
+    atomicAdd(&g_stamps[28], 1ull);
+  }
+#endif
+  for (int i = tid; i < nmol * ND; i += kThreads) y1[(size_t)mol0 * ND + i] = st.y[i];
+  if (tid < nmol) {
+    if (dlogp) dlogp[mol0 + tid] = st.lp[tid];
+    if (nfe_out) nfe_out[mol0 + tid] = st.nfe[tid];
+    if (status_out) status_out[mol0 + tid] = st.status[tid];
+  }
+}
+
+// one evaluation (and n_tangents JVPs) per molecule
+template <int NF, int NT, int L, int D>
+__global__ __launch_bounds__((Geo<NF, NT>::NTHR)) void vf_kernel(Net net, const float* __restrict__ x,
+                                                           const float* __restrict__ t,
+                                                           const int32_t* __restrict__ feat,
+                                                           const float* __restrict__ tan_in, int ntan, float* v,
+                                                           float* tan_out, int B) {
+  constexpr int kThreads = Geo<NF, NT>::NTHR;
+  extern __shared__ float smem[];
+  const int tid = threadIdx.x, MPW = net.MPW, ND = net.ND, N = net.N;
+  const Lds s = carve_lds<NT>(net, smem);
+  const SolverLds st = carve_solver(s.tail, MPW, ND);
+  const int mol0 = blockIdx.x * MPW;
+  const int nmol = min(MPW, B - mol0);
+  for (int i = tid; i < (int)(s.tail - smem); i += kThreads) smem[i] = 0.f;
+  __syncthreads();
+  for (int i = tid; i < MPW * ND; i += kThreads) st.ys[i] = (i / ND) < nmol ? x[(size_t)mol0 * ND + i] : 0.f;
+  for (int i = tid; i < MPW * N; i += kThreads) s.feat[i] = (i / N) < nmol ? feat[(size_t)mol0 * N + i] : 0;
+  if (tid < MPW) st.ts[tid] = tid < nmol ? t[mol0 + tid] : 0.f;
+  __syncthreads();
+  if constexpr (NT == 0) {
+    egnn_eval<NF, 0, L, D>(net, s, st.ys, st.ts, nullptr, st.vout, nullptr);
+    for (int i = tid; i < nmol * ND; i += kThreads) v[(size_t)mol0 * ND + i] = st.vout[i];
+  } else {
+    for (int k = 0; k < ntan; ++k) {
+      for (int i = tid; i < MPW * ND; i += kThreads) {
+        const int m = i / ND, c = i - m * ND;
+        st.tin[i] = m < nmol ? tan_in[((size_t)(mol0 + m) * ntan + k) * ND + c] : 0.f;
+      }
+      __syncthreads();
+      egnn_eval<NF, 1, L, D>(net, s, st.ys, st.ts, st.tin, st.vout, st.tout);
+      for (int i = tid; i < nmol * ND; i += kThreads) {
+        const int m = i / ND, c = i - m * ND;
+        tan_out[((size_t)(mol0 + m) * ntan + k) * ND + c] = st.tout[i];
+        if (k == 0 && v) v[(size_t)mol0 * ND + i] = st.vout[i];
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// ---- templated launchers (one instantiation per compiled shape and tangent flag) ----
+template <int NF, int NT, int L, int D>
+hipError_t launch_integrate(const Net& net, size_t lds, const SolveP& sp, const float* y0, const int32_t* feat,
+                            const float* eps, float* y1, float* dlogp, int32_t* nfe, int32_t* status, int B,
+                            hipStream_t stream) {
+  auto k = integrate_kernel<NF, NT, L, D>;
+  hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  const int grid = (B + net.MPW - 1) / net.MPW;
+  hipLaunchKernelGGL(k, dim3(grid), dim3(Geo<NF, NT>::NTHR), lds, stream, net, sp, y0, feat, eps, y1, dlogp, nfe,
+                     status, B);
+  return hipGetLastError();
+}
+
+template <int NF, int NT, int L, int D>
+hipError_t launch_vf(const Net& net, size_t lds, const float* x, const float* t, const int32_t* feat,
+                     const float* tan_in, int ntan, float* v, float* tan_out, int B, hipStream_t stream) {
+  auto k = vf_kernel<NF, NT, L, D>;
+  hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  const int grid = (B + net.MPW - 1) / net.MPW;
+  hipLaunchKernelGGL(k, dim3(grid), dim3(Geo<NF, NT>::NTHR), lds, stream, net, x, t, feat, tan_in, ntan, v, tan_out,
+                     B);
+  return hipGetLastError();
+}
+
+// compiled shapes: (M, L, D) with tangent support where registers allow (M <= 128).  __graft_entry__.build()
+// reads these two lists to compile one ecnf_part.hip translation unit per shape.
+#ifdef ECNF_DEV_LJ13_ONLY   // experiment builds (tools/build_variants.sh): the LJ13 shape only
+#define ECNF_SHAPES(X) X(128, 3, 3)
+#define ECNF_SHAPES_PRIMAL_ONLY(X)
+#else
+#define ECNF_SHAPES(X)  \
+  X(128, 3, 3)          \
+  X(128, 3, 2)          \
+  X(128, 2, 3)          \
+  X(128, 2, 2)          \
+  X(64, 2, 3)           \
+  X(64, 2, 2)           \
+  X(64, 3, 3)           \
+  X(64, 3, 2)
+
+#define ECNF_SHAPES_PRIMAL_ONLY(X) \
+  X(256, 4, 3)                     \
+  X(256, 3, 3)
+#endif
+
+
+// explicit instantiation (EXT = template) or instantiation declaration (EXT = extern template) of one shape
+#define ECNF_INST_SHAPE(EXT, m, l, d, NTV)                                                                    \
+  EXT hipError_t launch_integrate<m / 32, NTV, l, d>(const Net&, size_t, const SolveP&, const float*,         \
+                                                     const int32_t*, const float*, float*, float*, int32_t*, \
+                                                     int32_t*, int, hipStream_t);                             \
+  EXT hipError_t launch_vf<m / 32, NTV, l, d>(const Net&, size_t, const float*, const float*, const int32_t*, \
+                                              const float*, int, float*, float*, int, hipStream_t);
+
+}  // namespace ecnf
