@@ -115,7 +115,7 @@ struct Net {
 // ---------------------------------------------------------------------------------------------------
 enum StampSlot {
   kStPrologue = 0, kStNodeDense, kStPGemm, kStEdge, kStNodeUpd, kStPhiH, kStEpilogue, kStSolver,
-  kStEdgeChainE, kStEdgeTail, kStEdgeLayer1, kStCount
+  kStEdgeChainE, kStEdgeTail, kStEdgeLayer1, kStEdgeAgg, kStEdgePhiXIn, kStEdgePhiX, kStCount
 };
 #ifdef ECNF_STAMPS
 __device__ unsigned long long g_stamps[32];
@@ -371,7 +371,10 @@ __device__ __forceinline__ void node_task_split(const float* X1, int ldx1, int K
                                                 const unsigned* __restrict__ Wpk, float winv,
                                                 const float* __restrict__ bias, bool act, const float* resid, int ldr, float* Y, int ldy, int RP,
                                                 int nvalid, int jb, int ct, int lane) {
-  constexpr int PFA = 2;   // k-steps of A fragments in flight ahead of the MFMAs
+#ifndef ECNF_NODE_PFA
+#define ECNF_NODE_PFA 2
+#endif
+  constexpr int PFA = ECNF_NODE_PFA;   // k-steps of A fragments in flight ahead of the MFMAs
   jb = __builtin_amdgcn_readfirstlane(jb);   // uniform: buffer-load offsets in SGPRs (no waterfall loops)
   ct = __builtin_amdgcn_readfirstlane(ct);
   const int kk = lane >> 5, li = lane & 31;
@@ -409,35 +412,40 @@ __device__ __forceinline__ void node_task_split(const float* X1, int ldx1, int K
 #pragma unroll
       for (int p = 0; p < kPieces; ++p) w[a][p] = wload(rsrc, voff, (((jb + a) * nks + ks) * kPieces + p) * kPieceBytes);
   };
+  // A fragments: a ring of S = PFA + 1 k-step slots; the load of k-step ks + PFA is issued (clamped to the last
+  // k-step, so the main loop has no branches) before the MFMAs of k-step ks and pinned there by a sched_barrier,
+  // so PFA k-steps of MFMAs cover its latency
+  constexpr int S = PFA + 1;
   float bv[8];
-  u32x4 wa[PFA][NA][kPieces];
+  u32x4 wa[S][NA][kPieces];
   bload(0, bv);
+  static_for<PFA>([&](auto Ic) { aload(min((int)decltype(Ic)::value, nks - 1), wa[decltype(Ic)::value]); });
+  auto kstep = [&](int ks, auto Ic) {
+    constexpr int i = decltype(Ic)::value;
+    aload(min(ks + PFA, nks - 1), wa[(i + PFA) % S]);
+    u32x4 B[kPieces];
 #pragma unroll
-  for (int i = 0; i < PFA; ++i)
-    if (i < nks) aload(i, wa[i]);
-  for (int ks = 0; ks < nks; ks += PFA) {
+    for (int e = 0; e < 4; ++e) {
+      unsigned pc[kPieces];
+      split_pair(bv[2 * e], bv[2 * e + 1], pc);
 #pragma unroll
-    for (int i = 0; i < PFA; ++i) {
-      if (ks + i < nks) {
-        u32x4 B[kPieces];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          unsigned pc[kPieces];
-          split_pair(bv[2 * e], bv[2 * e + 1], pc);
-#pragma unroll
-          for (int p = 0; p < kPieces; ++p) B[p][e] = pc[p];
-        }
-        if (ks + i + 1 < nks) bload(ks + i + 1, bv);
-#pragma unroll
-        for (int a = 0; a < NA; ++a)
-          static_for<kTerms>([&](auto Tc) {
-            constexpr int t = decltype(Tc)::value;
-            acc[a] = mfma_split(wa[i][a][term_w(t)], B[term_x(t)], acc[a]);
-          });
-        if (ks + i + PFA < nks) aload(ks + i + PFA, wa[i]);
-      }
+      for (int p = 0; p < kPieces; ++p) B[p][e] = pc[p];
     }
-  }
+    bload(min(ks + 1, nks - 1), bv);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int a = 0; a < NA; ++a)
+      static_for<kTerms>([&](auto Tc) {
+        constexpr int t = decltype(Tc)::value;
+        acc[a] = mfma_split(wa[i][a][term_w(t)], B[term_x(t)], acc[a]);
+      });
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  int ks = 0;
+  for (; ks + S <= nks; ks += S) static_for<S>([&](auto Ic) { kstep(ks + decltype(Ic)::value, Ic); });
+  static_for<S>([&](auto Ic) {
+    if (ks + (int)decltype(Ic)::value < nks) kstep(ks + decltype(Ic)::value, Ic);
+  });
 #pragma unroll
   for (int a = 0; a < NA; ++a)
 #pragma unroll
@@ -850,6 +858,7 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
     STAMP_LANE0(s, kStEdgeChainE, t_sub);
     edge_tail<NF, NT, L, D>(net, bw, s, acc, acc, valid, rr, r, dr, length, dlength, lane,
                             [&](f32x16 (&m)[NF], f32x16 (&)[NF]) {
+                              STAMP_LANE0(s, kStEdgeAgg, t_sub);
                               // phi_x layers 1..L on the (ungated) messages
                               static_for<NF>([&](auto Fc) {
                                 constexpr int fb = decltype(Fc)::value;
@@ -859,7 +868,9 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
                                 });
                               });
                               const unsigned* Wx = launder_uniform(bw.Ws + (size_t)(L - 1) * SplitPlan<NF, 1>::GL * kGroupU32);
+                              STAMP_LANE0(s, kStEdgePhiXIn, t_sub);
                               chain_split<NF, L>(XA, XB, m, Wx, s.vecs + (L - 1) * NF * 32, ix, lane);
+                              STAMP_LANE0(s, kStEdgePhiX, t_sub);
                             });
     STAMP_LANE0(s, kStEdgeTail, t_sub);
     return;

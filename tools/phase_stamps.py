@@ -14,7 +14,8 @@ from ecnf_amd import CONFIGS, init_params, _lib  # noqa: E402
 from ecnf_amd.engine import EcnfHandle, SolveOptions  # noqa: E402
 
 NAMES = ["prologue", "node_dense", "p_gemm", "edge", "node_update", "phi_h", "epilogue", "solver",
-         "edge_chain_e(w0)", "edge_tail(w0)", "edge_layer1(w0)"]
+         "edge_chain_e(w0)", "edge_shift(w0)", "edge_layer1(w0)", "edge_gate_agg(w0)", "edge_phix_in(w0)",
+         "edge_phix_chain(w0)"]
 name = sys.argv[1] if len(sys.argv) > 1 else "lj13"
 B = int(sys.argv[2]) if len(sys.argv) > 2 else 1024
 cfg = CONFIGS[name]
