@@ -243,7 +243,8 @@ int choose_mpw(const ecnf_cfg& c, int NT, int* mpw_out, size_t* lds_out, int* rp
   int best_rp = 0;
   for (int m = 1; m <= 32; ++m) {
     const int RP = 32 * ((m * N + 31) / 32);
-    const int floats = (NT ? lds_eval_floats<1>(N, D, H, T, M, m, RP) : lds_eval_floats<0>(N, D, H, T, M, m, RP)) +
+    const bool vec = kSplitChain && !NT && M <= 128;   // Geo<NF, NT>::kSplit
+    const int floats = (NT ? lds_eval_floats<1>(N, D, H, T, M, m, RP, vec) : lds_eval_floats<0>(N, D, H, T, M, m, RP, vec)) +
                        solver_lds_floats(m, N * D);
     const size_t bytes = (size_t)floats * 4;
     if (bytes > 160 * 1024) break;

@@ -126,7 +126,7 @@ __global__ __launch_bounds__((Geo<NF, NT>::NTHR)) void integrate_kernel(Net net,
   constexpr int kThreads = Geo<NF, NT>::NTHR;
   extern __shared__ float smem[];
   const int tid = threadIdx.x, MPW = net.MPW, ND = net.ND, N = net.N;
-  const Lds s = carve_lds<NT>(net, smem);
+  const Lds s = carve_lds<NT, Geo<NF, NT>::kSplit>(net, smem);
   const SolverLds st = carve_solver(s.tail, MPW, ND);
   const int mol0 = blockIdx.x * MPW;
   const int nmol = min(MPW, B - mol0);
@@ -363,7 +363,7 @@ __global__ __launch_bounds__((Geo<NF, NT>::NTHR)) void vf_kernel(Net net, const 
   constexpr int kThreads = Geo<NF, NT>::NTHR;
   extern __shared__ float smem[];
   const int tid = threadIdx.x, MPW = net.MPW, ND = net.ND, N = net.N;
-  const Lds s = carve_lds<NT>(net, smem);
+  const Lds s = carve_lds<NT, Geo<NF, NT>::kSplit>(net, smem);
   const SolverLds st = carve_solver(s.tail, MPW, ND);
   const int mol0 = blockIdx.x * MPW;
   const int nmol = min(MPW, B - mol0);

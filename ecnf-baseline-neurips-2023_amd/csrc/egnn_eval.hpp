@@ -163,14 +163,24 @@ struct Lds {
 
 __host__ __device__ inline int align4(int n) { return (n + 3) & ~3; }
 
+// Leading dimensions of the node-row buffers.  fp32 node GEMMs (VEC = false) read one column per lane: odd
+// strides, conflict-free.  Split node GEMMs and the phi_e layer-1 gathers (VEC = true) read / write 16 B per lane
+// (ds_read_b128 / ds_write_b128): strides that are multiples of 4 floats with an odd multiple, so 16 consecutive
+// rows cover all 64 banks.
+__host__ __device__ inline int ld_node(int k, int odd_pad, bool vec) {
+  if (!vec) return k + odd_pad;
+  const int a = align4(k);
+  return ((a >> 2) & 1) ? a : a + 4;
+}
+
 template <int NT>
-__host__ __device__ inline int lds_eval_floats(int N, int D, int H, int T, int M, int MPW, int RP) {
+__host__ __device__ inline int lds_eval_floats(int N, int D, int H, int T, int M, int MPW, int RP, bool vec) {
   const int R = RP * (1 + NT);
   int n = 0;
-  n += align4(R * (H + T + 1));
-  n += align4(R * (H + 1));
-  n += align4(R * (2 * M + 3));
-  n += align4(R * (M + 1));
+  n += align4(R * ld_node(H + T, 1, vec));
+  n += align4(R * ld_node(H, 1, vec));
+  n += align4(R * ld_node(2 * M, 3, vec));
+  n += align4(R * ld_node(M, 1, vec));
   n += 3 * align4(R * D);
   n += align4(2 * MPW * D);
   n += align4(MPW * T);
@@ -182,15 +192,15 @@ __host__ __device__ inline int lds_eval_floats(int N, int D, int H, int T, int M
   return n;
 }
 
-template <int NT>
+template <int NT, bool VEC>
 __device__ inline Lds carve_lds(const Net& net, float* base) {
   Lds s;
   const int R = net.RP * (1 + NT);
   float* p = base;
-  s.hin = p;  s.ld_hin = net.H + net.T + 1; p += align4(R * s.ld_hin);
-  s.hb = p;   s.ld_hb = net.H + 1;          p += align4(R * s.ld_hb);
-  s.P = p;    s.ld_P = 2 * net.M + 3;       p += align4(R * s.ld_P);
-  s.macc = p; s.ld_m = net.M + 1;           p += align4(R * s.ld_m);
+  s.hin = p;  s.ld_hin = ld_node(net.H + net.T, 1, VEC); p += align4(R * s.ld_hin);
+  s.hb = p;   s.ld_hb = ld_node(net.H, 1, VEC);          p += align4(R * s.ld_hb);
+  s.P = p;    s.ld_P = ld_node(2 * net.M, 3, VEC);       p += align4(R * s.ld_P);
+  s.macc = p; s.ld_m = ld_node(net.M, 1, VEC);           p += align4(R * s.ld_m);
   s.xc = p;    p += align4(R * net.D);
   s.xc0 = p;   p += align4(R * net.D);
   s.dxacc = p; p += align4(R * net.D);
@@ -398,9 +408,14 @@ __device__ __forceinline__ void node_task_split(const float* X1, int ldx1, int K
     const float* src = first ? X1 + n * ldx1 : X2 + n * ldx2;
     const int c0 = 16 * (first ? ks : ks - nks1) + 8 * kk;
     const int K = first ? K1 : K2;
-    if (c0 + 8 <= K) {
+    if (c0 + 8 <= K) {   // 16-B aligned (ld_node with VEC): two ds_read_b128
+      const f32x4 lo = *reinterpret_cast<const f32x4*>(src + c0);
+      const f32x4 hi = *reinterpret_cast<const f32x4*>(src + c0 + 4);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = src[c0 + j];
+      for (int j = 0; j < 4; ++j) {
+        v[j] = lo[j];
+        v[4 + j] = hi[j];
+      }
     } else {
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = (c0 + j < K) ? src[c0 + j] : 0.f;
@@ -450,7 +465,23 @@ __device__ __forceinline__ void node_task_split(const float* X1, int ldx1, int K
   for (int a = 0; a < NA; ++a)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[a][r] = fmaf(acc[a][r], winv, bq[a][r >> 2][r & 3]);
-  node_epilogue<0, NA>(acc, accT, act, resid, ldr, Y, ldy, RP, nvalid, jb, n, kk);
+  // epilogue with 16-B LDS accesses: registers 4q..4q+3 are 4 consecutive output features
+  if (n < nvalid) {
+#pragma unroll
+    for (int a = 0; a < NA; ++a)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int j = (jb + a) * 32 + 8 * q + 4 * kk;
+        f32x4 y;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float t = acc[a][4 * q + e];
+          y[e] = act ? t * sigmoidf_(t) : t;
+        }
+        if (resid) y += *reinterpret_cast<const f32x4*>(resid + n * ldr + j);
+        *reinterpret_cast<f32x4*>(Y + n * ldy + j) = y;
+      }
+  }
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -835,12 +866,14 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
       constexpr int fb = decltype(Fc)::value;
       static_for<4>([&](auto Qc) {
         constexpr int q = decltype(Qc)::value;
-        const f32x4 w = *reinterpret_cast<const f32x4*>(s.vecs + (2 * L - 1) * (NF * 32) + fb * 32 + 8 * q + 4 * kk);
+        const int row = fb * 32 + 8 * q + 4 * kk;   // 4 consecutive features: 16-B LDS reads
+        const f32x4 w = *reinterpret_cast<const f32x4*>(s.vecs + (2 * L - 1) * (NF * 32) + row);
+        const f32x4 ps = *reinterpret_cast<const f32x4*>(Ps + row);
+        const f32x4 pr = *reinterpret_cast<const f32x4*>(Pr + row);
         static_for<2>([&](auto Hc) {
           constexpr int e = 2 * decltype(Hc)::value;
-          const int row = fb * 32 + 8 * q + 4 * kk + e;
-          const float u0 = Ps[row] + Pr[row] + len2 * w[e];   // log2 domain (silu_u)
-          const float u1 = Ps[row + 1] + Pr[row + 1] + len2 * w[e + 1];
+          const float u0 = ps[e] + pr[e] + len2 * w[e];   // log2 domain (silu_u)
+          const float u1 = ps[e + 1] + pr[e + 1] + len2 * w[e + 1];
           put_pair<NF, fb, 4 * q + e>(XA, silu_u(u0), silu_u(u1));
         });
       });
@@ -1025,7 +1058,7 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
     STAMP(s, kStNodeUpd);
     // phi_h = MLP((M,)*L + (H,)) on [m_i | h], residual (egnn.py:105-111)
     float* Q0 = s.P;
-    float* Q1 = s.P + (M + 1);
+    float* Q1 = s.P + (kSplitG ? M + 4 : M + 1);   // 16-B aligned rows for the split node GEMMs
     node_gemm<NT, kNW, kSplitG>(s.macc, s.ld_m, M, s.hb, s.ld_hb, H, bw.Wh[0], bw.Wh_s[0], bw.hinv[0], M, bw.bh[0], M, true, nullptr, 0, Q0, s.ld_P, RP,
                   nvalid, wave, lane);
     __syncthreads();
