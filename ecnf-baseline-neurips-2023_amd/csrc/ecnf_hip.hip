@@ -66,6 +66,102 @@ __global__ void base_log_prob_kernel(const float* __restrict__ y, float* out, in
   out[bb] = -0.5f * r2 + log_norm + ildj;
 }
 
+// -log_p = energy of the LJ / DW targets (leonard_jones.py:10-27, double_well.py:9-19), one thread per molecule.
+// The reference sums f(d) over the N(N-1) ordered pairs; each unordered pair is visited once here and counted twice.
+__global__ void target_log_prob_kernel(ecnf_target t, const float* __restrict__ x, float* log_p, int B) {
+  const int bb = blockIdx.x * blockDim.x + threadIdx.x;
+  if (bb >= B) return;
+  const int N = t.n_nodes, D = t.dim;
+  const float* xb = x + (size_t)bb * N * D;
+  float pair = 0.f;
+  for (int i = 0; i < N; ++i)
+    for (int j = i + 1; j < N; ++j) {
+      float x2 = 0.f;
+      for (int d = 0; d < D; ++d) {
+        const float v = xb[j * D + d] - xb[i * D + d];
+        x2 += v * v;
+      }
+      const float dist = sqrtf(x2 == 0.f ? 1.0f : x2);   // safe_norm (numerical.py:7-10)
+      float f;
+      if (t.kind == ECNF_TARGET_LJ) {
+        const float q = t.r / dist, q2 = q * q, q6 = q2 * q2 * q2;
+        f = q6 * q6 - 2.0f * q6;
+      } else {
+        const float u = dist - t.d0, u2 = u * u;
+        f = t.a * u + t.b * u2 + t.c * u2 * u2;
+      }
+      pair += 2.0f * f;
+    }
+  float e;
+  if (t.kind == ECNF_TARGET_LJ) {
+    float com[3] = {0.f, 0.f, 0.f};
+    for (int i = 0; i < N; ++i)
+      for (int d = 0; d < D; ++d) com[d] += xb[i * D + d];
+    for (int d = 0; d < D; ++d) com[d] /= (float)N;
+    float h = 0.f;
+    for (int i = 0; i < N; ++i)
+      for (int d = 0; d < D; ++d) {
+        const float v = xb[i * D + d] - com[d];
+        h += v * v;
+      }
+    e = t.epsilon / (2.0f * t.tau) * pair + t.harmonic_coef * h;
+  } else {
+    e = pair / t.tau / 2.0f;
+  }
+  log_p[bb] = -e;
+}
+
+// log-sum-exp partials (max, sum exp(s v - max)) for s = +1, -1, +2 and the count, one workgroup: online
+// rescaling per thread, then a tree over the workgroup in LDS
+constexpr int kLseThreads = 1024;
+__device__ __forceinline__ void lse_push(float& m, float& s, float v) {
+  if (v > m) {
+    s = s * __expf(m - v) + 1.0f;
+    m = v;
+  } else {
+    s += __expf(v - m);
+  }
+}
+__device__ __forceinline__ void lse_merge(float& m, float& s, float m2, float s2) {
+  if (m2 > m) {
+    s = s * __expf(m - m2) + s2;
+    m = m2;
+  } else if (m2 > -INFINITY) {
+    s += s2 * __expf(m2 - m);
+  }
+}
+__global__ __launch_bounds__(kLseThreads) void lse_partials_kernel(const float* __restrict__ v,
+                                                                   const float* __restrict__ mask, int n, float* out) {
+  __shared__ float red[7][kLseThreads];
+  float m[3] = {-INFINITY, -INFINITY, -INFINITY}, sm[3] = {0.f, 0.f, 0.f}, cnt = 0.f;
+  const float sc[3] = {1.0f, -1.0f, 2.0f};
+  for (int i = threadIdx.x; i < n; i += kLseThreads) {
+    if (mask && !(mask[i] > 0.f)) continue;
+    cnt += 1.0f;
+    for (int k = 0; k < 3; ++k) lse_push(m[k], sm[k], sc[k] * v[i]);
+  }
+  const int tid = threadIdx.x;
+  for (int k = 0; k < 3; ++k) {
+    red[2 * k][tid] = m[k];
+    red[2 * k + 1][tid] = sm[k];
+  }
+  red[6][tid] = cnt;
+  __syncthreads();
+  for (int w = kLseThreads / 2; w > 0; w >>= 1) {
+    if (tid < w) {
+      for (int k = 0; k < 3; ++k) {
+        float mm = red[2 * k][tid], ss = red[2 * k + 1][tid];
+        lse_merge(mm, ss, red[2 * k][tid + w], red[2 * k + 1][tid + w]);
+        red[2 * k][tid] = mm;
+        red[2 * k + 1][tid] = ss;
+      }
+      red[6][tid] += red[6][tid + w];
+    }
+    __syncthreads();
+  }
+  if (tid < 7) out[tid] = red[tid][0];
+}
+
 }  // namespace ecnf
 
 // =====================================================================================================
@@ -651,6 +747,28 @@ int ecnf_base_log_prob(ecnf_handle* h, const float* y, float* log_p, int32_t bat
   HIP_TRY(hipSetDevice(h->device));
   hipLaunchKernelGGL(base_log_prob_kernel, dim3((batch + 255) / 256), dim3(256), 0, (hipStream_t)stream, y, log_p,
                      batch, h->cfg.n_nodes, h->cfg.dim, h->cfg.base_scale);
+  HIP_TRY(hipGetLastError());
+  return ECNF_OK;
+}
+
+int ecnf_target_log_prob(const ecnf_target* t, const float* x, float* log_p, int32_t batch, void* stream) {
+  if (!t) return fail(ECNF_E_INVALID, "target is NULL");
+  if (t->kind != ECNF_TARGET_LJ && t->kind != ECNF_TARGET_DW) return fail(ECNF_E_INVALID, "unknown target kind");
+  if (t->n_nodes < 2 || t->dim < 1 || t->dim > 3) return fail(ECNF_E_INVALID, "target needs n_nodes >= 2, 1 <= dim <= 3");
+  if (!(t->tau > 0.f)) return fail(ECNF_E_INVALID, "target tau must be > 0");
+  if (batch < 0) return fail(ECNF_E_INVALID, "batch < 0");
+  if (batch == 0) return ECNF_OK;
+  if (!x || !log_p) return fail(ECNF_E_INVALID, "NULL argument");
+  hipLaunchKernelGGL(target_log_prob_kernel, dim3((batch + 255) / 256), dim3(256), 0, (hipStream_t)stream, *t, x, log_p,
+                     batch);
+  HIP_TRY(hipGetLastError());
+  return ECNF_OK;
+}
+
+int ecnf_lse_partials(const float* v, const float* mask, int32_t n, float* out, void* stream) {
+  if (n < 0) return fail(ECNF_E_INVALID, "n < 0");
+  if (!out || (n > 0 && !v)) return fail(ECNF_E_INVALID, "NULL argument");
+  hipLaunchKernelGGL(lse_partials_kernel, dim3(1), dim3(kLseThreads), 0, (hipStream_t)stream, v, mask, n, out);
   HIP_TRY(hipGetLastError());
   return ECNF_OK;
 }

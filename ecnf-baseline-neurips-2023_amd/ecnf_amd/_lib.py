@@ -21,8 +21,10 @@ CHAIN_FP32_MFMA, CHAIN_SPLIT_BF16, CHAIN_SPLIT_F16 = 0, 1, 2
 EXPORTED_SYMBOLS = (
     "ecnf_abi_version", "ecnf_last_error", "ecnf_param_count", "ecnf_create", "ecnf_destroy",
     "ecnf_vector_field", "ecnf_vf_jvp", "ecnf_integrate", "ecnf_base_sample", "ecnf_base_log_prob",
-    "ecnf_molecules_per_workgroup", "ecnf_chain_arithmetic",
+    "ecnf_molecules_per_workgroup", "ecnf_chain_arithmetic", "ecnf_target_log_prob", "ecnf_lse_partials",
 )
+
+TARGET_LJ, TARGET_DW = 0, 1
 
 
 class EcnfCfg(ctypes.Structure):
@@ -51,6 +53,22 @@ class EcnfSolveOpts(ctypes.Structure):
         ("atol", ctypes.c_float),
         ("dtmin", ctypes.c_float),
         ("max_steps", ctypes.c_int32),
+    ]
+
+
+class EcnfTarget(ctypes.Structure):
+    _fields_ = [
+        ("kind", ctypes.c_int32),
+        ("n_nodes", ctypes.c_int32),
+        ("dim", ctypes.c_int32),
+        ("epsilon", ctypes.c_float),
+        ("tau", ctypes.c_float),
+        ("r", ctypes.c_float),
+        ("harmonic_coef", ctypes.c_float),
+        ("a", ctypes.c_float),
+        ("b", ctypes.c_float),
+        ("c", ctypes.c_float),
+        ("d0", ctypes.c_float),
     ]
 
 
@@ -90,6 +108,9 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
         "ecnf_base_sample": ([P, P, P, I32, P], ctypes.c_int),
         "ecnf_base_log_prob": ([P, P, P, I32, P], ctypes.c_int),
         "ecnf_molecules_per_workgroup": ([P, I32, ctypes.POINTER(I32)], ctypes.c_int),
+        "ecnf_chain_arithmetic": ([P, I32, ctypes.POINTER(I32)], ctypes.c_int),
+        "ecnf_target_log_prob": ([ctypes.POINTER(EcnfTarget), P, P, I32, P], ctypes.c_int),
+        "ecnf_lse_partials": ([P, P, I32, P, P], ctypes.c_int),
     }
     for name, (argtypes, restype) in sig.items():
         fn = getattr(lib, name)

@@ -66,6 +66,31 @@ def masked_mean(values: torch.Tensor, mask: Optional[torch.Tensor] = None) -> to
     return torch.where(acc[1] == 0, torch.zeros_like(acc[0]), acc[0] / torch.clamp(acc[1], min=1.0))
 
 
+def combine_partials(p: torch.Tensor) -> torch.Tensor:
+    """Global [LSE(v), LSE(-v), LSE(2v), count] (fp64) from every rank's float[7] log-sum-exp partials
+    (targets.lse_partials / ecnf_lse_partials): one MAX all-reduce of the three maxima, then one SUM all-reduce of
+    the rescaled sums and the count."""
+    p = p.detach().to(torch.float64).reshape(7)
+    m_local = p[[0, 2, 4]]
+    m = _allreduce(m_local.clone(), dist.ReduceOp.MAX)
+    m0 = torch.where(torch.isfinite(m), m, torch.zeros_like(m))
+    scale = torch.where(torch.isfinite(m_local), torch.exp(m_local - m0), torch.zeros_like(m_local))
+    s = _allreduce(torch.cat([p[[1, 3, 5]] * scale, p[6:7]]), dist.ReduceOp.SUM)
+    return torch.cat([m0 + torch.log(s[:3]), s[3:]])
+
+
+def ess_from_device(log_w: torch.Tensor, mask: Optional[torch.Tensor] = None):
+    """(forward ESS, reverse ESS) of the global log_w from the HIP log-sum-exp partials of each rank's shard
+    (ecnf_lse_partials) and two scalar all-reduces.  Forward ESS follows evaluation.py:10-22 (masked);
+    reverse ESS setup_training.py:182 (over the unmasked entries)."""
+    from .targets import lse_partials
+    g = combine_partials(lse_partials(log_w, mask))
+    lse, lse_neg, lse_2, n = g[0], g[1], g[2], g[3]
+    fwd = torch.exp(-(lse_neg - torch.log(n)) - (lse - torch.log(n)))
+    rev = torch.exp(2 * lse - lse_2) / n
+    return fwd, rev
+
+
 def forward_ess(log_w: torch.Tensor, mask: Optional[torch.Tensor] = None) -> torch.Tensor:
     """evaluation.py:10-22: exp(-(LSE(-log_w) - log n) - (LSE(log_w) - log n))."""
     lw = log_w.detach().to(torch.float64).reshape(-1)

@@ -17,6 +17,10 @@
  *   ecnf_base_sample             <- cnf.sample_base (distrax Transformed._sample_n)
  *                                   zero_com_base.py:16-19,88-93 + build_cnf.py:46-61
  *   ecnf_base_log_prob           <- cnf.log_prob_base  zero_com_base.py:21-24,64-84 + build_cnf.py:50-57
+ *   ecnf_target_log_prob         <- target log_prob_fn (-energy) of LJ13 / DW4   
+ *                                   ecnf/targets/target_energy/leonard_jones.py:10-35, double_well.py:9-28
+ *   ecnf_lse_partials            <- the log-sum-exp reductions behind forward / reverse ESS  (section 8f, rank 2)
+ *                                   ecnf/train/evaluation.py:10-22, setup_training.py:182
  *   ecnf_last_error              <- the chex / diffrax exceptions (trace-time asserts, max_steps)
  *
  * Conventions
@@ -130,6 +134,29 @@ int ecnf_molecules_per_workgroup(ecnf_handle* h, int32_t with_tangent, int32_t* 
 #define ECNF_CHAIN_SPLIT_BF16 1
 #define ECNF_CHAIN_SPLIT_F16 2
 int ecnf_chain_arithmetic(ecnf_handle* h, int32_t with_tangent, int32_t* mode);
+
+/* ---- targets and eval reductions (no handle needed) ---- */
+enum ecnf_target_kind { ECNF_TARGET_LJ = 0, ECNF_TARGET_DW = 1 };
+
+/* Target energy parameters.  LJ (leonard_jones.py:10-27): epsilon, tau, r (scalar; the reference's per-node r
+ * array is not supported), harmonic_coef.  DW (double_well.py:9-19): a, b, c, d0, tau.  Defaults are the
+ * reference's keyword defaults (LJ: 1, 1, 1, 0.5; DW: 0, -4, 0.9, 4, 1). */
+typedef struct ecnf_target {
+  int32_t kind;      /* ecnf_target_kind */
+  int32_t n_nodes;
+  int32_t dim;
+  float epsilon, tau, r, harmonic_coef;  /* LJ */
+  float a, b, c, d0;                     /* DW (tau shared) */
+} ecnf_target;
+
+/* log_p[i] = -energy(x[i]) for x [batch, n_nodes*dim] (log_prob_fn of the target).  Pair distances use
+ * safe_norm (1 for coincident atoms) and the ordered-pair sum of the reference (each pair counted twice). */
+int ecnf_target_log_prob(const ecnf_target* t, const float* x, float* log_p, int32_t batch, void* stream);
+
+/* One workgroup reduces v[0..n) (entries with mask[i] <= 0 skipped when mask != NULL) to log-sum-exp partials
+ * for the scales s = +1, -1, +2:  out[2k] = max_i s v_i,  out[2k+1] = sum_i exp(s v_i - out[2k]),  out[6] = count.
+ * out is a DEVICE float[7].  Ranks combine partials with one MAX and one SUM all-reduce (ecnf_amd.distributed). */
+int ecnf_lse_partials(const float* v, const float* mask, int32_t n, float* out, void* stream);
 
 /* Thread-local description of the last error ("" when none). */
 const char* ecnf_last_error(void);

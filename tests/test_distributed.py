@@ -19,6 +19,28 @@ def _free_port():
         return s.getsockname()[1]
 
 
+def _np_partials(v, mask=None):
+    """The float[7] output contract of ecnf_lse_partials (include/ecnf.h), restated in numpy for host-side tests of
+    the cross-rank combine: (max s v, sum exp(s v - max)) for s = +1, -1, +2 over unmasked entries, then count."""
+    v = np.asarray(v, np.float64)
+    if mask is not None:
+        v = v[np.asarray(mask) > 0]
+    out = []
+    for s in (1.0, -1.0, 2.0):
+        if v.size:
+            m = (s * v).max()
+            out += [m, np.exp(s * v - m).sum()]
+        else:
+            out += [-np.inf, 0.0]
+    return torch.tensor(out + [float(v.size)], dtype=torch.float32)
+
+
+def _ess_from_partials(p):
+    g = D.combine_partials(p)
+    lse, lse_neg, lse_2, n = (float(x) for x in g)
+    return np.exp(-(lse_neg - np.log(n)) - (lse - np.log(n))), np.exp(2 * lse - lse_2) / n
+
+
 def _worker(rank, world, port, log_w, mask, q, out_q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -34,6 +56,8 @@ def _worker(rank, world, port, log_w, mask, q, out_q):
             "lse": float(D.logsumexp(lw)),
             "gathered": D.all_gather_rows(torch.from_numpy(q[lo:hi]).reshape(-1, 1)).numpy().ravel(),
             "z": D.global_normal(9, 3, 7, *D.shard_bounds(9, rank, world), device="cpu").numpy(),
+            "ess_partials": _ess_from_partials(_np_partials(log_w[lo:hi], mask[lo:hi])),
+            "ress_partials": _ess_from_partials(_np_partials(log_w[lo:hi]))[1],
         }
         out_q.put((rank, res))
     finally:
@@ -65,6 +89,9 @@ def test_gloo_reductions_match_single_process(world):
         m = log_w.max()
         assert abs(res["lse"] - (m + np.log(np.exp(log_w - m).sum()))) < 1e-10
         np.testing.assert_array_equal(res["gathered"], q)
+        # the device-partials path (fp32 partials, as ecnf_lse_partials returns them)
+        assert abs(res["ess_partials"][0] - O.forward_ess(log_w, mask)) < 1e-5
+        assert abs(res["ress_partials"] - O.reverse_ess(log_w)) < 1e-5
     z_full = D.global_normal(9, 3, 7, 0, 9, device="cpu").numpy()
     np.testing.assert_array_equal(np.concatenate([results[r]["z"] for r in range(world)]), z_full)
 
@@ -84,3 +111,13 @@ def test_single_process_reductions_without_init():
     assert abs(float(D.reverse_ess(lw)) - O.reverse_ess(lw.numpy())) < 1e-12
     assert abs(float(D.forward_ess(lw)) - O.forward_ess(lw.numpy())) < 1e-12
     assert float(D.masked_mean(lw, torch.zeros(3))) == 0.0
+
+
+def test_combine_partials_single_process_and_empty_shard():
+    rng = np.random.default_rng(3)
+    lw = rng.standard_normal(50) * 4.0
+    fwd, rev = _ess_from_partials(_np_partials(lw))
+    assert abs(fwd - O.forward_ess(lw)) < 1e-5 and abs(rev - O.reverse_ess(lw)) < 1e-5
+    # an empty shard contributes (-inf, 0) partials and must not poison the combine
+    g = D.combine_partials(_np_partials(np.zeros(0)))
+    assert float(g[3]) == 0.0
