@@ -622,6 +622,9 @@ int ecnf_create(const ecnf_cfg* cfg, const float* params, size_t n_floats, int d
     if (shape_supported(c, NT) && choose_mpw(c, NT, &mpw, &lds, &rp) == ECNF_OK) {
       n.MPW = mpw;
       n.RP = rp;
+      // split kernels store segment parts; the continuation rows [MPW][EP/32][ld_m] overlay hin (egnn_eval.hpp)
+      const bool vec = kSplitChain && !NT && M <= 128;
+      n.cross = vec && (size_t)mpw * (n.EP / 32) * ld_node(M, 1, true) <= (size_t)rp * ld_node(H + T, 1, true);
       h->lds[NT] = lds;
     } else {
       n.MPW = 0;

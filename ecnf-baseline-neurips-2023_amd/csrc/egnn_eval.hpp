@@ -103,6 +103,7 @@ struct Net {
   float fs;       // EGNN final_scaling
   float nn1;      // avg_num_neighbours = N - 1
   float sqrt_nn1; // sqrt(N - 1) in fp32
+  int cross;      // split kernels: message segment parts are stored, not atomically added (Lds::cross)
   float freqs[kMaxHalfT];
   const float* emb;
   BlockW blk[kMaxBlocks];
@@ -157,6 +158,8 @@ struct Lds {
   float* temb;               // [MPW][T]
   float* vecs;               // [(2L-1) + 3][M] this block's chain biases, w_d, w_g, w_x (staged once per block)
   int*   feat;               // [MPW][N]
+  float* cross;              // [MPW][EP/32][ld_m] continuation parts of receiver segments that cross a tile
+                             // boundary (aliases hin, which is dead during the edge phase; split kernels)
   float* tail;               // first free float (solver state follows)
   ECNF_STAMP_DECL
 };
@@ -211,6 +214,7 @@ __device__ inline Lds carve_lds(const Net& net, float* base) {
 #ifdef ECNF_STAMPS
   s.stamps = reinterpret_cast<unsigned long long*>(p); p += 64;
 #endif
+  s.cross = s.hin;
   s.tail = p;
   return s;
 }
@@ -730,9 +734,9 @@ __device__ __forceinline__ void edge_shift(const Net& net, const BlockW& bw, con
 // gate, message aggregation, phi_x torso + output, shifts (egnn.py:81-104); `m` holds the messages
 template <int NF, int NT, int L, int D, typename PhiX>
 __device__ __forceinline__ void edge_tail(const Net& net, const BlockW& bw, const Lds& s, f32x16 (&X)[NF],
-                                          f32x16 (&XT)[NF], bool valid, int rr, const float (&r)[D],
-                                          const float (&dr)[D], float length, float dlength, int lane,
-                                          PhiX&& phi_x) {
+                                          f32x16 (&XT)[NF], bool valid, int rr, float* agg_dst,
+                                          const float (&r)[D], const float (&dr)[D], float length, float dlength,
+                                          int lane, PhiX&& phi_x) {
   f32x16(&m)[NF] = X;
   f32x16(&mT)[NF] = XT;
   const int kk = lane >> 5, li = lane & 31;
@@ -768,8 +772,16 @@ __device__ __forceinline__ void edge_tail(const Net& net, const BlockW& bw, cons
     sc.sum_many<16>(v);
 #endif
     if (writer) {
+      if (agg_dst) {
+        // the segment part's sums as 4 x 16-B stores into its own row (no atomics; combined in the node update)
 #pragma unroll
-      for (int r16 = 0; r16 < 16; ++r16) lds_add(&s.macc[rr * s.ld_m + fb * 32 + acc_row(r16, kk)], v[r16]);
+        for (int q = 0; q < 4; ++q)
+          *reinterpret_cast<f32x4*>(agg_dst + fb * 32 + 8 * q + 4 * kk) =
+              f32x4{v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
+      } else {
+#pragma unroll
+        for (int r16 = 0; r16 < 16; ++r16) lds_add(&s.macc[rr * s.ld_m + fb * 32 + acc_row(r16, kk)], v[r16]);
+      }
     }
     if constexpr (NT) {
 #pragma unroll
@@ -826,6 +838,15 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
   if (sd >= N) sd -= N;
   const int mrow = valid ? mol : 0;
   const int rr = mrow * N + i, rs = mrow * N + sd;   // receiver / sender rows (graph.py:10-13)
+  // split kernels: the row this lane's receiver-segment part is stored to — macc for the part in the tile where
+  // the segment starts, the cross buffer (one row per molecule tile) for its continuation in the next tile
+  float* agg_dst = nullptr;
+  if constexpr (Geo<NF, NT>::kSplit) {
+    if (net.cross) {
+      const int tloc = tile - mrow * (net.EP >> 5);
+      agg_dst = tloc == ((i * nn1) >> 5) ? s.macc + rr * s.ld_m : s.cross + (mrow * (net.EP >> 5) + tloc) * s.ld_m;
+    }
+  }
 #ifdef ECNF_STAMPS
   unsigned long long t_sub = __builtin_amdgcn_s_memtime();
 #endif
@@ -889,7 +910,7 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
     });
     chain_split<NF, L - 1>(XA, XB, acc, Ws, s.vecs, ie, lane);
     STAMP_LANE0(s, kStEdgeChainE, t_sub);
-    edge_tail<NF, NT, L, D>(net, bw, s, acc, acc, valid, rr, r, dr, length, dlength, lane,
+    edge_tail<NF, NT, L, D>(net, bw, s, acc, acc, valid, rr, agg_dst, r, dr, length, dlength, lane,
                             [&](f32x16 (&m)[NF], f32x16 (&)[NF]) {
                               STAMP_LANE0(s, kStEdgeAgg, t_sub);
                               // phi_x layers 1..L on the (ungated) messages
@@ -944,7 +965,7 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
   const float* We = launder_uniform(bw.We);
   chain_segment<NF, NT, L - 1>(X, XT, We, s.vecs, lane);
   STAMP_LANE0(s, kStEdgeChainE, t_sub);
-  edge_tail<NF, NT, L, D>(net, bw, s, X, XT, valid, rr, r, dr, length, dlength, lane,
+  edge_tail<NF, NT, L, D>(net, bw, s, X, XT, valid, rr, agg_dst, r, dr, length, dlength, lane,
                           [&](f32x16 (&Y)[NF], f32x16 (&YT)[NF]) {
                             const float* Wx = launder_uniform(bw.We + (L - 1) * NF * NF * 1024);
                             chain_segment<NF, NT, L>(Y, YT, Wx, s.vecs + (L - 1) * NF * 32, lane);
@@ -1051,10 +1072,25 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
     for (int idx = tid; idx < R * M; idx += kNT) {
       const int row = idx / M, c = idx - row * M;
       float mv = s.macc[row * s.ld_m + c];
-      if constexpr (kSplitG) mv *= -0.69314718055994531f;   // log2-domain messages (chain_split.hpp, silu_u)
+      if constexpr (kSplitG) {
+        if (net.cross && row < nvalid) {   // add the continuation part of a segment that crosses a tile boundary
+          const int m = row / N, i = row - m * N, nn1 = N - 1;
+          const int first = (i * nn1) >> 5, last = (i * nn1 + nn1 - 1) >> 5;
+          if (last != first) mv += s.cross[(m * (net.EP >> 5) + last) * s.ld_m + c];
+        }
+        mv *= -0.69314718055994531f;   // log2-domain messages (chain_split.hpp, silu_u)
+      }
       s.macc[row * s.ld_m + c] = mv / net.sqrt_nn1;
     }
     __syncthreads();
+    if constexpr (kSplitG) {
+      if (net.cross) {   // the cross buffer overlaid hin's time-embedding columns: restore them
+        for (int idx = tid; idx < nvalid * T; idx += kNT) {
+          const int row = idx / T, c = idx - row * T;
+          s.hin[row * s.ld_hin + H + c] = s.temb[(row / N) * T + c];
+        }
+      }
+    }
     STAMP(s, kStNodeUpd);
     // phi_h = MLP((M,)*L + (H,)) on [m_i | h], residual (egnn.py:105-111)
     float* Q0 = s.P;
@@ -1062,9 +1098,11 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
     node_gemm<NT, kNW, kSplitG>(s.macc, s.ld_m, M, s.hb, s.ld_hb, H, bw.Wh[0], bw.Wh_s[0], bw.hinv[0], M, bw.bh[0], M, true, nullptr, 0, Q0, s.ld_P, RP,
                   nvalid, wave, lane);
     __syncthreads();
-    for (int idx = tid; idx < R * M; idx += kNT) {
-      const int row = idx / M, c = idx - row * M;
-      s.macc[row * s.ld_m + c] = 0.f;
+    if (!(kSplitG && net.cross)) {   // atomically accumulated aggregates restart from +0
+      for (int idx = tid; idx < R * M; idx += kNT) {
+        const int row = idx / M, c = idx - row * M;
+        s.macc[row * s.ld_m + c] = 0.f;
+      }
     }
     for (int l = 1; l < L; ++l) {
       node_gemm<NT, kNW, kSplitG>(Q0, s.ld_P, M, nullptr, 0, 0, bw.Wh[l], bw.Wh_s[l], bw.hinv[l], M, bw.bh[l], M, true, nullptr, 0, Q1, s.ld_P, RP,
