@@ -565,7 +565,16 @@ int ecnf_create(const ecnf_cfg* cfg, const float* params, size_t n_floats, int d
     for (int l = 0; l <= L; ++l) {
       const int out_f = l == L ? H : M, in_f = l == 0 ? M + H : M;
       o.Wh[l] = pk.put(b.hk[l], (size_t)in_f * out_f);
-      o.Wh_s[l] = put_split_node(b.hk[l], in_f, out_f, &o.hinv[l]);
+      if (l == 0) {
+        // the split kernels' aggregated messages arrive unscaled and in the log2 domain: fold -ln2 / sqrt(N-1)
+        // (egnn.py:104) into the message rows 0..M-1 of phi_h.0 (the node update then only combines segment parts)
+        std::vector<float> w0(b.hk[0], b.hk[0] + (size_t)in_f * out_f);
+        const float f = kNegLn2 / std::sqrt((float)(c.n_nodes - 1));
+        for (size_t i = 0; i < (size_t)M * out_f; ++i) w0[i] *= f;
+        o.Wh_s[l] = put_split_node(w0.data(), in_f, out_f, &o.hinv[l]);
+      } else {
+        o.Wh_s[l] = put_split_node(b.hk[l], in_f, out_f, &o.hinv[l]);
+      }
       o.bh[l] = pk.put(b.hb[l], out_f);
     }
   }
@@ -624,7 +633,18 @@ int ecnf_create(const ecnf_cfg* cfg, const float* params, size_t n_floats, int d
       n.RP = rp;
       // split kernels store segment parts; the continuation rows [MPW][EP/32][ld_m] overlay hin (egnn_eval.hpp)
       const bool vec = kSplitChain && !NT && M <= 128;
-      n.cross = vec && (size_t)mpw * (n.EP / 32) * ld_node(M, 1, true) <= (size_t)rp * ld_node(H + T, 1, true);
+      n.cross = vec && (size_t)mpw * (n.EP / 32) * ld_node(M, 1, true) <= (size_t)rp * ld_node(H + T, 1, true) &&
+                n.EP / 32 <= kMaxTilesPerMol;
+      // segments (receiver i: edges i(N-1) .. i(N-1)+N-2) that a tile boundary 32t splits; their continuation part
+      // sits in cross row t of the molecule
+      n.ncross = 0;
+      const int nn1 = c.n_nodes - 1;
+      for (int t = 1; n.cross && t < n.EP / 32; ++t)
+        if (32 * t < n.E && (32 * t) % nn1 != 0) {
+          n.xs_i[n.ncross] = (unsigned char)((32 * t) / nn1);
+          n.xs_t[n.ncross] = (unsigned char)t;
+          ++n.ncross;
+        }
       h->lds[NT] = lds;
     } else {
       n.MPW = 0;

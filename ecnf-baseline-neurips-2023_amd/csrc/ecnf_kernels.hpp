@@ -66,6 +66,10 @@ __device__ inline SolverLds carve_solver(float* p, int MPW, int ND) {
   return st;
 }
 
+__device__ __forceinline__ float uniform_f(float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, x)));
+}
+
 __device__ inline float clip_end(float tn, float tau1) { return tn > tau1 - 1e-6f ? tau1 : tn; }
 
 // one evaluation of the joint field g(tau, y) = dir * f(dir * tau, y) at (st.ts, st.ys) for every molecule
@@ -74,7 +78,7 @@ template <int NF, int NT, int L, int D>
 __device__ __forceinline__ void joint_field(const Net& net, const Lds& s, const SolverLds& st, const SolveP& sp,
                                             float* kx_out, float* kl_out) {
   constexpr int kThreads = Geo<NF, NT>::NTHR;
-  const int tid = threadIdx.x, MPW = net.MPW, ND = net.ND;
+  const int tid = opaque_tid(), MPW = net.MPW, ND = net.ND;
   // NT == 0: one primal eval; Hutchinson: one JVP along eps; exact: ND JVPs along e_k (trace of J)
   const int nrep = (NT == 0 || sp.div == ECNF_DIV_HUTCHINSON) ? 1 : ND;
   if (tid < MPW) st.divv[tid] = 0.f;
@@ -156,7 +160,8 @@ __global__ __launch_bounds__((Geo<NF, NT>::NTHR)) void integrate_kernel(Net net,
   __syncthreads();
 
   // Euler: ConstantStepSize, all molecules share the (uniform, register-held) time grid
-  float e_tau = sp.tau0, e_tn = clip_end(sp.tau0 + sp.dt0, sp.tau1), e_h = 0.f;
+  // (wave-uniform values pinned to SGPRs with readfirstlane: as VGPRs they are live across every eval and spill)
+  float e_tau = sp.tau0, e_tn = uniform_f(clip_end(sp.tau0 + sp.dt0, sp.tau1)), e_h = 0.f;
   int e_steps = 0;
   int phase = sp.solver == ECNF_SOLVER_EULER ? kEuler : (sp.adaptive ? kInit0 : kFsal);
   int stage = 1;
@@ -169,6 +174,7 @@ __global__ __launch_bounds__((Geo<NF, NT>::NTHR)) void integrate_kernel(Net net,
   }
 #endif
   while (true) {
+    const int tid = opaque_tid();   // shadows the kernel-level tid: nothing per-thread stays live across an eval
     STAMP(s, kStSolver);
     // ------------------------------------------------ inputs of this evaluation
     float* kx_out;
@@ -179,7 +185,7 @@ __global__ __launch_bounds__((Geo<NF, NT>::NTHR)) void integrate_kernel(Net net,
         if (tid < nmol) st.status[tid] = ECNF_E_MAX_STEPS;
         break;
       }
-      e_h = e_tn - e_tau;
+      e_h = uniform_f(e_tn - e_tau);
       for (int i = tid; i < MPW * ND; i += kThreads) st.ys[i] = st.y[i];
       if (tid < MPW) st.ts[tid] = sp.dirf * e_tau;
       kx_out = st.kx; kl_out = st.kl;
@@ -219,7 +225,7 @@ __global__ __launch_bounds__((Geo<NF, NT>::NTHR)) void integrate_kernel(Net net,
       for (int i = tid; i < MPW * ND; i += kThreads) st.y[i] = st.y[i] + e_h * st.kx[i];
       if (tid < MPW) st.lp[tid] = st.lp[tid] + e_h * st.kl[tid];
       e_tau = e_tn;
-      e_tn = clip_end(e_tau + sp.dt0, sp.tau1);
+      e_tn = uniform_f(clip_end(e_tau + sp.dt0, sp.tau1));
     } else if (phase == kInit0) {
       // Hairer's initial step, part 1 (diffrax _select_initial_step)
       if (tid < MPW) {

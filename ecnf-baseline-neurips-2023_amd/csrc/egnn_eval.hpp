@@ -54,6 +54,7 @@ struct Geo {
 constexpr int kMaxBlocks = 10;
 constexpr int kMaxPhiH = 5;     // L + 1 <= 5
 constexpr int kMaxHalfT = 8;    // T <= 16
+constexpr int kMaxTilesPerMol = 32;   // EP / 32 for N <= 33
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -108,6 +109,9 @@ struct Net {
   float nn1;      // avg_num_neighbours = N - 1
   float sqrt_nn1; // sqrt(N - 1) in fp32
   int cross;      // split kernels: message segment parts are stored, not atomically added (Lds::cross)
+  int ncross;     // receiver segments per molecule that cross a tile boundary (split kernels with cross)
+  unsigned char xs_i[kMaxTilesPerMol];   // ... their receiver atom i
+  unsigned char xs_t[kMaxTilesPerMol];   // ... and the molecule tile that holds their continuation part
   float freqs[kMaxHalfT];
   const float* emb;
   BlockW blk[kMaxBlocks];
@@ -247,6 +251,24 @@ __device__ __forceinline__ const T* launder_uniform(const T* p) {
   uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
   asm volatile("" : "+s"(lo), "+s"(hi));
   return reinterpret_cast<const T*>(((uint64_t)hi << 32) | lo);
+}
+
+// threadIdx.x through an empty asm: per-thread indices and LDS addresses derived from it are recomputed where they
+// are used (a few VALU) instead of being hoisted out of the solver loop and kept live across the edge phase, whose
+// tiles need every register (hoisted, they spill to scratch)
+__device__ __forceinline__ int opaque_tid() {
+  int t = threadIdx.x;
+  asm volatile("" : "+v"(t));
+  return t;
+}
+
+// an LDS base pointer through an empty asm (wave-uniform): the carve-up offsets are recomputed per use site on the
+// scalar unit instead of occupying SGPRs (and their VGPR spill lanes) across the whole solve
+__device__ __forceinline__ float* opaque_smem(float* p) {
+  uint32_t v = (uint32_t)reinterpret_cast<uintptr_t>(p);
+  v = __builtin_amdgcn_readfirstlane(v);
+  asm volatile("" : "+s"(v));
+  return reinterpret_cast<float*>((uintptr_t)v);
 }
 
 __device__ __forceinline__ f32x4 ldg4(const float* p, int idx4) { return gptr4(p)[idx4]; }
@@ -986,7 +1008,7 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
                           float* v_out, float* tan_out) {
   constexpr int kNW = Geo<NF, NT>::NW, kNT = Geo<NF, NT>::NTHR;
   constexpr bool kSplitG = Geo<NF, NT>::kSplit;
-  const int tid = threadIdx.x, lane = tid & 63;
+  const int tid = opaque_tid(), lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: task indices stay in SGPRs
   const int N = net.N, H = net.H, T = net.T, M = NF * 32, RP = net.RP, MPW = net.MPW, ND = net.ND;
   const int nvalid = MPW * N;
@@ -1073,18 +1095,24 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
       s.xc[idx] += s.dxacc[idx] / net.nn1;
       s.dxacc[idx] = 0.f;
     }
-    for (int idx = tid; idx < R * M; idx += kNT) {
-      const int row = idx / M, c = idx - row * M;
-      float mv = s.macc[row * s.ld_m + c];
-      if constexpr (kSplitG) {
-        if (net.cross && row < nvalid) {   // add the continuation part of a segment that crosses a tile boundary
-          const int m = row / N, i = row - m * N, nn1 = N - 1;
-          const int first = (i * nn1) >> 5, last = (i * nn1 + nn1 - 1) >> 5;
-          if (last != first) mv += s.cross[(m * (net.EP >> 5) + last) * s.ld_m + c];
+    if constexpr (kSplitG) {
+      // the split phi_h.0 weights carry the message scale -ln2 / sqrt(N-1) (log2-domain messages, chain_split.hpp;
+      // egnn.py:104), so only the continuation parts of the segments that cross a tile boundary are added here:
+      // one (molecule, crossing) row per wave trip, wave-uniform indices
+      if (net.cross) {
+        const int nx = net.ncross, tpm = net.EP >> 5;
+        for (int j = wave; j < MPW * nx; j += kNW) {
+          const int m = j / nx, q = j - m * nx;
+          float* dst = s.macc + (m * N + net.xs_i[q]) * s.ld_m;
+          const float* src = s.cross + (m * tpm + net.xs_t[q]) * s.ld_m;
+          for (int c = lane; c < M; c += 64) dst[c] += src[c];
         }
-        mv *= -0.69314718055994531f;   // log2-domain messages (chain_split.hpp, silu_u)
       }
-      s.macc[row * s.ld_m + c] = mv / net.sqrt_nn1;
+    } else {
+      for (int idx = tid; idx < R * M; idx += kNT) {
+        const int row = idx / M, c = idx - row * M;
+        s.macc[row * s.ld_m + c] = s.macc[row * s.ld_m + c] / net.sqrt_nn1;
+      }
     }
     __syncthreads();
     if constexpr (kSplitG) {

@@ -1,0 +1,87 @@
+"""Throughput of every ecnf_integrate mode on the BASELINE.json configs (one MI355X), for DESIGN.md section 5.
+
+Each line: config, batch, solver, divergence, ms per launch (median of REPS HIP-event timings on the launch stream),
+molecules/s, mean NFE per molecule, and achieved algorithmic TFLOP/s counting (1 + tangents) x F per evaluation
+(F = bench.flops_per_eval; Hutchinson = 1 tangent, exact = N*D tangents).  Synthetic seeded inputs, flax-default
+random-init weights.  Usage: python tools/bench_paths.py [out.json]
+"""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "ecnf-baseline-neurips-2023_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+from bench import flops_per_eval  # noqa: E402
+from ecnf_amd import CONFIGS, init_params, _lib  # noqa: E402
+from ecnf_amd.engine import EcnfHandle, SolveOptions  # noqa: E402
+
+REPS = 3
+CASES = [
+    # config, batch, solver, step (None = adaptive PID), divergence, direction (sample 0->1 | logp 1->0)
+    ("lj13", 1024, "euler", 0.01, "none", "sample"),
+    ("lj13", 1024, "dopri5", 0.05, "none", "sample"),
+    ("lj13", 1024, "euler", 0.01, "hutchinson", "sample"),
+    ("lj13", 1024, "euler", 0.01, "exact", "logp"),
+    ("lj13", 8192, "euler", 0.01, "none", "sample"),
+    ("dw4", 1024, "euler", 0.01, "none", "sample"),
+    ("dw4", 1024, "dopri5", None, "hutchinson", "sample"),
+    ("aldp", 512, "dopri5", None, "none", "sample"),
+    ("aldp", 512, "dopri5", None, "hutchinson", "logp"),
+    ("qm9", 2048, "euler", 0.01, "none", "sample"),
+]
+DIV = {"none": _lib.DIV_NONE, "hutchinson": _lib.DIV_HUTCHINSON, "exact": _lib.DIV_EXACT}
+
+
+def run_case(name, B, solver, step, div, direction):
+    cfg = CONFIGS[name]
+    h = EcnfHandle(cfg, init_params(cfg, 0), 0)
+    g = torch.Generator("cuda").manual_seed(1234)
+    z = torch.randn((B, cfg.event_dim), device="cuda", generator=g)
+    x0 = h.base_sample(z)
+    feat = torch.arange(cfg.n_nodes, device="cuda", dtype=torch.int32) % cfg.n_features
+    feat = feat.expand(B, -1).contiguous()
+    eps = torch.randn((B, cfg.event_dim), device="cuda", generator=g) if div == "hutchinson" else None
+    o = SolveOptions(solver, step)
+    t0, t1 = (0.0, 1.0) if direction == "sample" else (1.0, 0.0)
+    h.integrate(x0, feat, t0, t1, o, DIV[div], eps, check_status=False)
+    stream = torch.cuda.current_stream()
+    ts = []
+    for _ in range(REPS):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        y1, dl, nfe, st = h.integrate(x0, feat, t0, t1, o, DIV[div], eps, check_status=False)
+        b.record(stream)
+        torch.cuda.synchronize()
+        ts.append(a.elapsed_time(b))
+    ms = sorted(ts)[len(ts) // 2]
+    nfe_mean = float(nfe.float().mean())
+    tangents = {"none": 0, "hutchinson": 1, "exact": cfg.event_dim}[div]
+    flop = B * nfe_mean * flops_per_eval(cfg) * (1 + tangents)
+    rec = {"config": name, "batch": B, "solver": solver, "step": step, "divergence": div, "direction": direction,
+           "ms": round(ms, 3), "molecules_per_s": round(B / ms * 1e3, 1), "nfe_mean": round(nfe_mean, 2),
+           "tflops": round(flop / ms / 1e9, 2), "bad_status": int((st != 0).sum()),
+           "finite": bool(torch.isfinite(y1).all())}
+    h.close()
+    return rec
+
+
+def main():
+    out = []
+    for case in CASES:
+        t = time.time()
+        rec = run_case(*case)
+        rec["wall_s"] = round(time.time() - t, 1)
+        print(json.dumps(rec), flush=True)
+        out.append(rec)
+    if len(sys.argv) > 1:
+        with open(sys.argv[1], "w") as f:
+            json.dump(out, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
