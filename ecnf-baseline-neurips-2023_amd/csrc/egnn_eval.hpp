@@ -762,10 +762,17 @@ template <int NF, int NT, int L, int D, typename PhiX>
 __device__ __forceinline__ void edge_tail(const Net& net, const BlockW& bw, const Lds& s, f32x16 (&X)[NF],
                                           f32x16 (&XT)[NF], bool valid, int rr, float* agg_dst,
                                           const float (&r)[D], const float (&dr)[D], float length, float dlength,
-                                          int lane, PhiX&& phi_x) {
+                                          int lane, bool agg, PhiX&& phi_x) {
   f32x16(&m)[NF] = X;
   f32x16(&mT)[NF] = XT;
   const int kk = lane >> 5, li = lane & 31;
+  SegScan sc;
+  sc.init(valid ? rr : -1, li);
+  const bool writer = valid && sc.tail;
+  const int RP = net.RP;
+  // the gate and the message aggregate only feed phi_h, i.e. h, which the last block's caller never reads (v depends
+  // on x alone, egnn.py:176-188): agg == false skips them (wave-uniform)
+  if (agg) {
   // gate e_ij = sigmoid(m_ij . w_g + b_g)  (egnn.py:99-101)
   float part = 0.f, partT = 0.f;
 #pragma unroll
@@ -785,10 +792,6 @@ __device__ __forceinline__ void edge_tail(const Net& net, const BlockW& bw, cons
   const float gT = NT ? g * (1.0f - g) * partT : 0.f;
 
   // m_i = scatter_sum(m_ij * e_ij) (the / sqrt(N-1) happens in the node update)   (egnn.py:102-104)
-  SegScan sc;
-  sc.init(valid ? rr : -1, li);
-  const bool writer = valid && sc.tail;
-  const int RP = net.RP;
 #pragma unroll
   for (int fb = 0; fb < NF; ++fb) {
     float v[16];
@@ -820,6 +823,7 @@ __device__ __forceinline__ void edge_tail(const Net& net, const BlockW& bw, cons
       }
     }
   }
+  }  // agg
 
   // phi_x torso (egnn.py:82) then its Dense(1) and the shifts
   phi_x(X, XT);
@@ -830,7 +834,7 @@ __device__ __forceinline__ void edge_tail(const Net& net, const BlockW& bw, cons
 
 // one 32-edge tile through phi_e / gate / phi_x  (egnn.py:72-95)
 template <int NF, int NT, int L, int D>
-__device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, const Lds& s, int tile, int lane) {
+__device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, const Lds& s, int tile, int lane, bool agg) {
   const int kk = lane >> 5, li = lane & 31;
 #ifdef ECNF_EXP_CHAIN_ONLY
   {  // timing experiment: the two chain segments alone, on synthetic activations, one LDS add as the sink
@@ -936,7 +940,7 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
     });
     chain_split<NF, L - 1>(XA, XB, acc, Ws, s.vecs, ie, lane);
     STAMP_LANE0(s, kStEdgeChainE, t_sub);
-    edge_tail<NF, NT, L, D>(net, bw, s, acc, acc, valid, rr, agg_dst, r, dr, length, dlength, lane,
+    edge_tail<NF, NT, L, D>(net, bw, s, acc, acc, valid, rr, agg_dst, r, dr, length, dlength, lane, agg,
                             [&](f32x16 (&m)[NF], f32x16 (&)[NF]) {
                               STAMP_LANE0(s, kStEdgeAgg, t_sub);
                               // phi_x layers 1..L on the (ungated) messages
@@ -991,7 +995,7 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
   const float* We = launder_uniform(bw.We);
   chain_segment<NF, NT, L - 1>(X, XT, We, s.vecs, lane);
   STAMP_LANE0(s, kStEdgeChainE, t_sub);
-  edge_tail<NF, NT, L, D>(net, bw, s, X, XT, valid, rr, agg_dst, r, dr, length, dlength, lane,
+  edge_tail<NF, NT, L, D>(net, bw, s, X, XT, valid, rr, agg_dst, r, dr, length, dlength, lane, agg,
                           [&](f32x16 (&Y)[NF], f32x16 (&YT)[NF]) {
                             const float* Wx = launder_uniform(bw.We + (L - 1) * NF * NF * 1024);
                             chain_segment<NF, NT, L>(Y, YT, Wx, s.vecs + (L - 1) * NF * 32, lane);
@@ -1053,6 +1057,11 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
   const int ntiles = (MPW * net.EP) >> 5;
   for (int k = 0; k < net.K; ++k) {
     const BlockW& bw = net.blk[k];
+    // fresh (opaque) thread indices per phase group: per-thread addresses of the node phases are then computed after
+    // the edge phase instead of being hoisted above it and kept live (spilled) through it
+    int tid = opaque_tid(), lane = tid & 63;
+    // the last block's h update (gate, aggregation, phi_h) is dead: the field is x_K - x_c - mean (egnn.py:176-188)
+    const bool need_h = k + 1 < net.K;
     // stage this block's chain biases and the w_d / w_g / w_x vectors in LDS (read by every edge tile)
     {
       const float* be = kSplitG ? bw.be_u : bw.be;
@@ -1087,13 +1096,23 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
 #else
     const int ntiles_run = ntiles;
 #endif
-    for (int tile = wave; tile < ntiles_run; tile += kNW) edge_tile<NF, NT, L, D>(net, bw, s, tile, lane);
+    {
+      const int elane = opaque_tid() & 63;
+      for (int tile = wave; tile < ntiles_run; tile += kNW) edge_tile<NF, NT, L, D>(net, bw, s, tile, elane, need_h);
+    }
     __syncthreads();
     STAMP(s, kStEdge);
+    tid = opaque_tid();
+    lane = tid & 63;
     // node update: x += shift_i / (N-1) (egnn.py:95,113); m_i /= sqrt(N-1) (egnn.py:104)
     for (int idx = tid; idx < R * D; idx += kNT) {
       s.xc[idx] += s.dxacc[idx] / net.nn1;
       s.dxacc[idx] = 0.f;
+    }
+    if (!need_h) {   // last block: no h update
+      __syncthreads();
+      STAMP(s, kStNodeUpd);
+      continue;
     }
     if constexpr (kSplitG) {
       // the split phi_h.0 weights carry the message scale -ln2 / sqrt(N-1) (log2-domain messages, chain_split.hpp;
