@@ -339,7 +339,7 @@ int choose_mpw(const ecnf_cfg& c, int NT, int* mpw_out, size_t* lds_out, int* rp
   int best_rp = 0;
   for (int m = 1; m <= 32; ++m) {
     const int RP = 32 * ((m * N + 31) / 32);
-    const bool vec = kSplitChain && !NT && M <= 128;   // Geo<NF, NT>::kSplit
+    const bool vec = kSplitChain && !NT && M <= 32 * kSplitMaxNF;   // Geo<NF, NT>::kSplit
     const int floats = (NT ? lds_eval_floats<1>(N, D, H, T, M, m, RP, vec) : lds_eval_floats<0>(N, D, H, T, M, m, RP, vec)) +
                        solver_lds_floats(m, N * D);
     const size_t bytes = (size_t)floats * 4;
@@ -632,7 +632,7 @@ int ecnf_create(const ecnf_cfg* cfg, const float* params, size_t n_floats, int d
       n.MPW = mpw;
       n.RP = rp;
       // split kernels store segment parts; the continuation rows [MPW][EP/32][ld_m] overlay hin (egnn_eval.hpp)
-      const bool vec = kSplitChain && !NT && M <= 128;
+      const bool vec = kSplitChain && !NT && M <= 32 * kSplitMaxNF;
       n.cross = vec && (size_t)mpw * (n.EP / 32) * ld_node(M, 1, true) <= (size_t)rp * ld_node(H + T, 1, true) &&
                 n.EP / 32 <= kMaxTilesPerMol;
       // segments (receiver i: edges i(N-1) .. i(N-1)+N-2) that a tile boundary 32t splits; their continuation part
@@ -678,7 +678,7 @@ int ecnf_molecules_per_workgroup(ecnf_handle* h, int32_t with_tangent, int32_t* 
 
 int ecnf_chain_arithmetic(ecnf_handle* h, int32_t with_tangent, int32_t* mode) {
   if (!h || !mode) return fail(ECNF_E_INVALID, "NULL argument");
-  const bool split = kSplitChain && !with_tangent && h->cfg.mlp_width <= 128;   // Geo<NF, NT>::kSplit
+  const bool split = kSplitChain && !with_tangent && h->cfg.mlp_width <= 32 * kSplitMaxNF;   // Geo<NF, NT>::kSplit
 #ifdef ECNF_SPLIT_BF16
   *mode = split ? ECNF_CHAIN_SPLIT_BF16 : ECNF_CHAIN_FP32_MFMA;
 #else

@@ -41,10 +41,15 @@ constexpr bool kSplitChain = true;
 // Waves per workgroup.  Split primal kernels: 8 waves = 2 per SIMD (<= 256 registers each): one wave's VALU and
 // LDS phases (activations, gate / aggregation scans, layer-1 gathers) overlap the other wave's MFMA chain
 // (measured 31.5 -> 28.6 ms at LJ13 over 4 waves with 512 registers).  fp32-MFMA chain, primal, M <= 128: 8 waves.
-// Tangent kernels and M = 256 carry twice the registers per tile: 4 waves.
+// Tangent kernels and the split M = 256 chain (QM9: 3 x 128 registers of split input / output / accumulators per
+// tile) need up to 512 registers: 4 waves, 1 per SIMD (QM9 B = 2048 Euler-100: fp32 MFMA 7203 ms -> split 2271 ms).
+#ifndef ECNF_SPLIT_MAX_NF
+#define ECNF_SPLIT_MAX_NF 8
+#endif
+constexpr int kSplitMaxNF = ECNF_SPLIT_MAX_NF;   // split chain up to M = 32 kSplitMaxNF
 template <int NF, int NT>
 struct Geo {
-  static constexpr bool kSplit = kSplitChain && NT == 0 && NF <= 4;
+  static constexpr bool kSplit = kSplitChain && NT == 0 && NF <= kSplitMaxNF;
 #ifndef ECNF_SPLIT_NW
 #define ECNF_SPLIT_NW 8
 #endif

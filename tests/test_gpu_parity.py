@@ -162,6 +162,19 @@ def test_euler_sample(name):
     assert (status.cpu().numpy() == 0).all()
 
 
+@pytest.mark.parametrize("name,B,steps", [("qm9", 3, 10), ("aldp", 5, 25)])
+def test_euler_sample_short(name, B, steps):
+    """Split-fp16 chain at M = 256 (QM9, 4 waves) and M = 64 (ALDP) over a short Euler trajectory; tolerance 1e-4."""
+    cfg = CONFIGS[name]
+    oc, params, h, z, x0, feat = setup(cfg, B=B)
+    dt = 1.0 / steps
+    y1, _, nfe, status = h.integrate(g(x0), g(feat, torch.int32), 0.0, 1.0, SolveOptions("euler", dt))
+    ref, nfe_ref = O.sample_cnf(params, oc, x0, feat, solver="euler", dt0=dt, dtype=np.float64)
+    assert np.abs(y1.cpu().numpy() - ref).max() <= 1e-4
+    assert (nfe.cpu().numpy() == steps).all() and (nfe_ref == steps).all()
+    assert (status.cpu().numpy() == 0).all()
+
+
 def test_dopri5_fixed_sample():
     cfg = CONFIGS["lj13"]
     oc, params, h, z, x0, feat = setup(cfg, B=6)

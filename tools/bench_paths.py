@@ -3,7 +3,7 @@
 Each line: config, batch, solver, divergence, ms per launch (median of REPS HIP-event timings on the launch stream),
 molecules/s, mean NFE per molecule, and achieved algorithmic TFLOP/s counting (1 + tangents) x F per evaluation
 (F = bench.flops_per_eval; Hutchinson = 1 tangent, exact = N*D tangents).  Synthetic seeded inputs, flax-default
-random-init weights.  Usage: python tools/bench_paths.py [out.json]
+random-init weights.  Usage: [ECNF_PATHS_ONLY=qm9,aldp] python tools/bench_paths.py [out.json]
 """
 import json
 import os
@@ -72,7 +72,10 @@ def run_case(name, B, solver, step, div, direction):
 
 def main():
     out = []
+    only = os.environ.get("ECNF_PATHS_ONLY")   # comma-separated config names
     for case in CASES:
+        if only and case[0] not in only.split(","):
+            continue
         t = time.time()
         rec = run_case(*case)
         rec["wall_s"] = round(time.time() - t, 1)
