@@ -201,10 +201,15 @@ __device__ __forceinline__ auto& pick(A& a, B& b) {
 #ifdef ECNF_SPLIT_WLDS
 __shared__ unsigned g_wlds_exp[8 * kPieces * 256];
 #endif
-template <int NF, int NL>
+// NT = 1 (forward-mode tangent, the divergence kernels): XAT / XBT / accT carry the tangent of every activation
+// through the same layers.  Each weight fragment feeds 2 kTerms MFMAs (primal and tangent interleaved); the
+// tangent of a layer is du = accT inv (no bias) and dy' = silu'(t) du = r (1 - ln2 u (1 - r)) du with the primal's
+// r = 1 / (1 + 2^u) (silu'(t) = sigma(t) (1 + t (1 - sigma(t))), t = -ln2 u).
+template <int NF, int NL, int NT = 0>
 __device__ __forceinline__ void chain_split(SplitX<NF>& XA, SplitX<NF>& XB, f32x16 (&acc)[NF],
                                             const unsigned* __restrict__ Wpk, const float* __restrict__ bias,
-                                            const ChainInv& inv, int lane) {
+                                            const ChainInv& inv, int lane, SplitX<NF>& XAT, SplitX<NF>& XBT,
+                                            f32x16 (&accT)[NF]) {
   using Plan = SplitPlan<NF, NL>;
   constexpr int GB = Plan::GB, GL = Plan::GL, G = Plan::G, NI = Plan::NI, PF = ECNF_SPLIT_PF;
   constexpr int GE = Plan::last_group() + 1;   // groups including the VALU-only tail
@@ -219,7 +224,7 @@ __device__ __forceinline__ void chain_split(SplitX<NF>& XA, SplitX<NF>& XB, f32x
 #pragma unroll
     for (int p = 0; p < kPieces; ++p) wbuf[gg][p] = wload(rsrc, voff, (gg * kPieces + p) * kPieceBytes);
   // per-item pipeline registers (SSA after unrolling: only live items occupy registers)
-  f32x2 bv[NI], uv[NI], ev[NI];
+  f32x2 bv[NI], uv[NI], ev[NI], dv[NI];
   static_for<Plan::count(0, 0)>([&](auto Kc) {
     constexpr int id = Plan::nth(0, 0, decltype(Kc)::value);
     bv[id] = *reinterpret_cast<const f32x2*>(lbias + Plan::bias_off(id));
@@ -253,14 +258,17 @@ __device__ __forceinline__ void chain_split(SplitX<NF>& XA, SplitX<NF>& XB, f32x
       auto& Xin = pick<l & 1>(XA, XB);
       const u32x4* A = wbuf[gg % (PF + 1)];
       const u32x4* B = Xin.v[fb][u];
+      const u32x4* BT = pick<l & 1>(XAT, XBT).v[fb][u];
       static_for<kTerms>([&](auto Tc) {
         constexpr int t = decltype(Tc)::value;
         constexpr int pa = term_w(t), pb = term_x(t);   // cross terms, smallest first
         if constexpr (fb == 0 && u == 0 && t == 0) {
           const f32x16 z = {};
           acc[jb] = mfma_split(A[pa], B[pb], z);
+          if constexpr (NT) accT[jb] = mfma_split(A[pa], BT[pb], z);
         } else {
           acc[jb] = mfma_split(A[pa], B[pb], acc[jb]);
+          if constexpr (NT) accT[jb] = mfma_split(A[pa], BT[pb], accT[jb]);
         }
       });
     }
@@ -285,6 +293,10 @@ __device__ __forceinline__ void chain_split(SplitX<NF>& XA, SplitX<NF>& XB, f32x
       uv[id][1] = fmaf(acc[it.j][r + 1], inv.v[it.l], bv[id][1]);
       ev[id][0] = __builtin_amdgcn_exp2f(uv[id][0]);
       ev[id][1] = __builtin_amdgcn_exp2f(uv[id][1]);
+      if constexpr (NT) {
+        dv[id][0] = accT[it.j][r] * inv.v[it.l];
+        dv[id][1] = accT[it.j][r + 1] * inv.v[it.l];
+      }
     });
     // stage B
     static_for<nB>([&](auto Kc) {
@@ -304,12 +316,24 @@ __device__ __forceinline__ void chain_split(SplitX<NF>& XA, SplitX<NF>& XB, f32x
         acc[it.j][2 * it.p] = y0;
         acc[it.j][2 * it.p + 1] = y1;
       }
+      if constexpr (NT) {
+        constexpr float kNegLn2 = -0.69314718055994531f;
+        const float d0 = ev[id][0] * fmaf(uv[id][0] * (1.0f - ev[id][0]), kNegLn2, 1.0f) * dv[id][0];
+        const float d1 = ev[id][1] * fmaf(uv[id][1] * (1.0f - ev[id][1]), kNegLn2, 1.0f) * dv[id][1];
+        if constexpr (it.l < NL - 1) {
+          put_pair<NF, it.j, 2 * it.p>(pick<(it.l + 1) & 1>(XAT, XBT), d0, d1);
+        } else {
+          accT[it.j][2 * it.p] = d0;
+          accT[it.j][2 * it.p + 1] = d1;
+        }
+      }
     });
 #endif
     if constexpr (mfma_group) {
       // schedule: weight loads, bias reads, then MFMA / VALU alternating
-      constexpr int nvalu = 4 * nA + 4 * nB + 3 * nC;
-      constexpr int per = (nvalu + kTerms - 1) / kTerms;
+      constexpr int nvalu = (4 + 2 * NT) * nA + 4 * nB + (3 + 13 * NT) * nC;
+      constexpr int nmfma = kTerms * (1 + NT);
+      constexpr int per = (nvalu + nmfma - 1) / nmfma;
 #ifndef ECNF_SPLIT_NO_SGB
 #if defined(ECNF_SPLIT_WLDS)
       if constexpr (gg + PF < G) __builtin_amdgcn_sched_group_barrier(0x100, kPieces, 0);
@@ -317,7 +341,7 @@ __device__ __forceinline__ void chain_split(SplitX<NF>& XA, SplitX<NF>& XB, f32x
       if constexpr (gg + PF < G) __builtin_amdgcn_sched_group_barrier(0x020, kPieces, 0);
 #endif
       if constexpr (nbias > 0) __builtin_amdgcn_sched_group_barrier(0x100, nbias, 0);
-      static_for<kTerms>([&](auto) {
+      static_for<nmfma>([&](auto) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
         if constexpr (per > 0) __builtin_amdgcn_sched_group_barrier(0x002, per, 0);
       });
@@ -325,4 +349,38 @@ __device__ __forceinline__ void chain_split(SplitX<NF>& XA, SplitX<NF>& XB, f32x
       __builtin_amdgcn_sched_barrier(0);
     }
   });
+}
+
+// primal-only chain (the tangent arguments alias the primal ones and are never touched)
+template <int NF, int NL>
+__device__ __forceinline__ void chain_split(SplitX<NF>& XA, SplitX<NF>& XB, f32x16 (&acc)[NF],
+                                            const unsigned* __restrict__ Wpk, const float* __restrict__ bias,
+                                            const ChainInv& inv, int lane) {
+  chain_split<NF, NL, 0>(XA, XB, acc, Wpk, bias, inv, lane, XA, XB, acc);
+}
+
+// the tangent kernels' chain segment on natural-domain fp32 activations (fp32-MFMA accumulator layout, as
+// chain_segment): X, XT -> log2 domain, split, NL dual layers, back to the natural domain in place.  Biases: the
+// log2-domain copies (the NT kernels stage be_u); weights: the same split fragments as the primal kernels.
+template <int NF, int NL>
+__device__ __forceinline__ void chain_split_tangent(f32x16 (&X)[NF], f32x16 (&XT)[NF], const unsigned* __restrict__ Wpk,
+                                                    const float* __restrict__ bias, const ChainInv& inv, int lane) {
+  constexpr float kNegLog2e = -1.4426950408889634f, kNegLn2 = -0.69314718055994531f;
+  SplitX<NF> XA, XB, XAT, XBT;
+  static_for<NF>([&](auto Fc) {
+    constexpr int fb = decltype(Fc)::value;
+    static_for<8>([&](auto Ic) {
+      constexpr int i = decltype(Ic)::value;
+      put_pair<NF, fb, 2 * i>(XA, kNegLog2e * X[fb][2 * i], kNegLog2e * X[fb][2 * i + 1]);
+      put_pair<NF, fb, 2 * i>(XAT, kNegLog2e * XT[fb][2 * i], kNegLog2e * XT[fb][2 * i + 1]);
+    });
+  });
+  chain_split<NF, NL, 1>(XA, XB, X, Wpk, bias, inv, lane, XAT, XBT, XT);
+#pragma unroll
+  for (int fb = 0; fb < NF; ++fb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      X[fb][r] *= kNegLn2;
+      XT[fb][r] *= kNegLn2;
+    }
 }

@@ -43,6 +43,11 @@ constexpr bool kSplitChain = true;
 // (measured 31.5 -> 28.6 ms at LJ13 over 4 waves with 512 registers).  fp32-MFMA chain, primal, M <= 128: 8 waves.
 // Tangent kernels and the split M = 256 chain (QM9: 3 x 128 registers of split input / output / accumulators per
 // tile) need up to 512 registers: 4 waves, 1 per SIMD (QM9 B = 2048 Euler-100: fp32 MFMA 7203 ms -> split 2271 ms).
+#ifdef ECNF_FP32_TANGENT_CHAIN
+constexpr bool kSplitTanChain = false;
+#else
+constexpr bool kSplitTanChain = kSplitChain;
+#endif
 #ifndef ECNF_SPLIT_MAX_NF
 #define ECNF_SPLIT_MAX_NF 8
 #endif
@@ -50,6 +55,8 @@ constexpr int kSplitMaxNF = ECNF_SPLIT_MAX_NF;   // split chain up to M = 32 kSp
 template <int NF, int NT>
 struct Geo {
   static constexpr bool kSplit = kSplitChain && NT == 0 && NF <= kSplitMaxNF;
+  // tangent kernels: the edge chains run split (chain_split_tangent); node GEMMs, layer 1 and the tail stay fp32
+  static constexpr bool kSplitT = kSplitTanChain && NT == 1 && NF <= 4;
 #ifndef ECNF_SPLIT_NW
 #define ECNF_SPLIT_NW 8
 #endif
@@ -997,6 +1004,23 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
   STAMP_LANE0(s, kStEdgeLayer1, t_sub);
   // phi_e layers 2..L.  The weight pointer is laundered through an empty asm so the (tile-invariant) weight
   // loads are not hoisted out of the tile loop into thousands of live registers.
+  if constexpr (Geo<NF, NT>::kSplitT) {
+    // split-fp16 chains with tangents (chain_split_tangent; the staged chain biases are the log2-domain copies)
+    ChainInv ie, ix;
+    static_for<2 * 4 - 1>([&](auto Lc) {
+      constexpr int l = decltype(Lc)::value;
+      ie.v[l] = l < L - 1 ? bw.cinv[l] : 1.0f;
+      ix.v[l] = l < L ? bw.cinv[L - 1 + l] : 1.0f;
+    });
+    chain_split_tangent<NF, L - 1>(X, XT, launder_uniform(bw.Ws), s.vecs, ie, lane);
+    STAMP_LANE0(s, kStEdgeChainE, t_sub);
+    edge_tail<NF, NT, L, D>(net, bw, s, X, XT, valid, rr, agg_dst, r, dr, length, dlength, lane, agg,
+                            [&](f32x16 (&Y)[NF], f32x16 (&YT)[NF]) {
+                              const unsigned* Wx =
+                                  launder_uniform(bw.Ws + (size_t)(L - 1) * SplitPlan<NF, 1>::GL * kGroupU32);
+                              chain_split_tangent<NF, L>(Y, YT, Wx, s.vecs + (L - 1) * NF * 32, ix, lane);
+                            });
+  } else {
   const float* We = launder_uniform(bw.We);
   chain_segment<NF, NT, L - 1>(X, XT, We, s.vecs, lane);
   STAMP_LANE0(s, kStEdgeChainE, t_sub);
@@ -1005,6 +1029,7 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
                             const float* Wx = launder_uniform(bw.We + (L - 1) * NF * NF * 1024);
                             chain_segment<NF, NT, L>(Y, YT, Wx, s.vecs + (L - 1) * NF * 32, lane);
                           });
+  }
   STAMP_LANE0(s, kStEdgeTail, t_sub);
 }
 
@@ -1069,7 +1094,7 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
     const bool need_h = k + 1 < net.K;
     // stage this block's chain biases and the w_d / w_g / w_x vectors in LDS (read by every edge tile)
     {
-      const float* be = kSplitG ? bw.be_u : bw.be;
+      const float* be = (kSplitG || Geo<NF, NT>::kSplitT) ? bw.be_u : bw.be;
       const float* wd = kSplitG ? bw.wd_u : bw.wd;
       const float* wg = kSplitG ? bw.wg_u : bw.wg;
       const float* wx = kSplitG ? bw.wx_u : bw.wx;
