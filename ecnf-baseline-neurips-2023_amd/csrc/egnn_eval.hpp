@@ -709,6 +709,27 @@ struct SegScan {
     const int nxt = __shfl_down(seg, 1, 32);
     tail = (li == 31) || (nxt != seg);
   }
+#ifndef ECNF_DPP_BUILTIN
+  // one fused v_fmac_f32_dpp per value and step (v += ok * v[lane - shift]).  The builtin form compiles to
+  // v_mov_b32_dpp + v_fmac_f32 + s_nop 0 per value (the DPP read of a just-written temp needs wait states), 3 issue
+  // slots instead of 1.  Wait states for the fused form: a value is re-read through DPP NV - 1 >= 2 instructions
+  // after its last write inside the scan, and the s_nop 1 in front covers the writes before it.  Row masks as the
+  // builtin form (row_bcast:15 writes rows 1 and 3 only; rows 0 and 2 keep v, where the builtin added ok * 0).
+  template <int NV>
+  __device__ __forceinline__ void sum_many(float (&v)[NV]) const {
+    static_assert(NV >= 3, "DPP wait states assume >= 3 interleaved values");
+    asm volatile("s_nop 1");
+#define ECNF_DPP_STEP(K, CTRL)                                                                          \
+    _Pragma("unroll") for (int i = 0; i < NV; ++i)                                                      \
+      asm volatile("v_fmac_f32_dpp %0, %0, %1 " CTRL " bank_mask:0xf bound_ctrl:1" : "+v"(v[i]) : "v"(okf[K]));
+    ECNF_DPP_STEP(0, "row_shr:1 row_mask:0xf")
+    ECNF_DPP_STEP(1, "row_shr:2 row_mask:0xf")
+    ECNF_DPP_STEP(2, "row_shr:4 row_mask:0xf")
+    ECNF_DPP_STEP(3, "row_shr:8 row_mask:0xf")
+    ECNF_DPP_STEP(4, "row_bcast:15 row_mask:0xa")
+#undef ECNF_DPP_STEP
+  }
+#else
   template <int NV>
   __device__ __forceinline__ void sum_many(float (&v)[NV]) const {
 #pragma unroll
@@ -722,6 +743,7 @@ struct SegScan {
 #pragma unroll
     for (int i = 0; i < NV; ++i) v[i] = fmaf(okf[4], dpp_f<0x142, 0xA>(v[i]), v[i]);
   }
+#endif
 };
 
 __device__ __forceinline__ void lds_add(float* p, float v) {
