@@ -549,7 +549,17 @@ int ecnf_create(const ecnf_cfg* cfg, const float* params, size_t n_floats, int d
     for (int cl = 0; cl < 2 * 4 - 1; ++cl) o.cinv[cl] = 1.0f;
     for (int cl = 0; cl < nchain; ++cl) {
       const float* W = cl < L - 1 ? b.ek[cl + 1] : b.tk[cl - (L - 1)];
+#ifdef ECNF_CHAIN_BIAS_INIT
+      // unscaled pieces: the chain adds the bias through the accumulator (chain_split.hpp); fp16 piece 0 must not
+      // overflow
+      float mx = 0.f;
+      for (size_t i = 0; i < (size_t)M * M; ++i) mx = std::max(mx, std::fabs(W[i]));
+      if (!(mx < 32768.f))
+        return fail(ECNF_E_UNSUPPORTED, "edge-MLP weight magnitude >= 2^15 does not fit the unscaled fp16 split");
+      const float sc = 1.0f;
+#else
       const float sc = split_scale(W, (size_t)M * M);
+#endif
       o.cinv[cl] = 1.0f / sc;
       pack_split_layer(W, M, sc, ws.data() + cl * split_layer);
     }

@@ -431,6 +431,9 @@ hipError_t launch_vf(const Net& net, size_t lds, const float* x, const float* t,
 #ifdef ECNF_DEV_LJ13_ONLY   // experiment builds (tools/build_variants.sh): the LJ13 shape only
 #define ECNF_SHAPES(X) X(128, 3, 3)
 #define ECNF_SHAPES_PRIMAL_ONLY(X)
+#elif defined(ECNF_DEV_M)       // experiment builds of one other shape (tools/build_timing.sh with DEVFLAGS)
+#define ECNF_SHAPES(X) X(ECNF_DEV_M, ECNF_DEV_L, ECNF_DEV_D)
+#define ECNF_SHAPES_PRIMAL_ONLY(X)
 #else
 #define ECNF_SHAPES(X)  \
   X(128, 3, 3)          \

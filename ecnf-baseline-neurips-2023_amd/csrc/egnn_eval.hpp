@@ -709,16 +709,30 @@ struct SegScan {
     const int nxt = __shfl_down(seg, 1, 32);
     tail = (li == 31) || (nxt != seg);
   }
+  // FUSED: the inline-asm form below (primal kernels); the builtin form otherwise
+  template <int NV, bool FUSED>
+  __device__ __forceinline__ void sum_many(float (&v)[NV]) const {
 #ifndef ECNF_DPP_BUILTIN
+    if constexpr (FUSED) {
+      sum_fused<NV>(v);
+      return;
+    }
+#endif
+    sum_builtin<NV>(v);
+  }
   // one fused v_fmac_f32_dpp per value and step (v += ok * v[lane - shift]).  The builtin form compiles to
   // v_mov_b32_dpp + v_fmac_f32 + s_nop 0 per value (the DPP read of a just-written temp needs wait states), 3 issue
-  // slots instead of 1.  Wait states for the fused form: a value is re-read through DPP NV - 1 >= 2 instructions
-  // after its last write inside the scan, and the s_nop 1 in front covers the writes before it.  Row masks as the
-  // builtin form (row_bcast:15 writes rows 1 and 3 only; rows 0 and 2 keep v, where the builtin added ok * 0).
+  // slots instead of 1.  Wait states for the fused form (the compiler's hazard recognizer does not look inside
+  // inline asm): a value is re-read through DPP NV - 1 >= 2 instructions after its last write inside the scan, and
+  // the s_nop 4 in front covers VALU writes of v (2 wait states) and an EXEC write just before the scan (5; e.g. the
+  // end of the tangent kernels' `if (writer)` stores).  Row masks as the builtin form (row_bcast:15 writes rows 1
+  // and 3 only; rows 0 and 2 keep v, where the builtin added ok * 0).
   template <int NV>
-  __device__ __forceinline__ void sum_many(float (&v)[NV]) const {
+  __device__ __forceinline__ void sum_fused(float (&v)[NV]) const {
     static_assert(NV >= 3, "DPP wait states assume >= 3 interleaved values");
-    asm volatile("s_nop 1");
+    // the scheduler must not sink the producers of v below the s_nop (volatile asm only orders asm statements)
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_nop 4");
 #define ECNF_DPP_STEP(K, CTRL)                                                                          \
     _Pragma("unroll") for (int i = 0; i < NV; ++i)                                                      \
       asm volatile("v_fmac_f32_dpp %0, %0, %1 " CTRL " bank_mask:0xf bound_ctrl:1" : "+v"(v[i]) : "v"(okf[K]));
@@ -728,10 +742,10 @@ struct SegScan {
     ECNF_DPP_STEP(3, "row_shr:8 row_mask:0xf")
     ECNF_DPP_STEP(4, "row_bcast:15 row_mask:0xa")
 #undef ECNF_DPP_STEP
+    __builtin_amdgcn_sched_barrier(0);
   }
-#else
   template <int NV>
-  __device__ __forceinline__ void sum_many(float (&v)[NV]) const {
+  __device__ __forceinline__ void sum_builtin(float (&v)[NV]) const {
 #pragma unroll
     for (int i = 0; i < NV; ++i) v[i] = fmaf(okf[0], dpp_f<0x111, 0xF>(v[i]), v[i]);
 #pragma unroll
@@ -743,7 +757,6 @@ struct SegScan {
 #pragma unroll
     for (int i = 0; i < NV; ++i) v[i] = fmaf(okf[4], dpp_f<0x142, 0xA>(v[i]), v[i]);
   }
-#endif
 };
 
 __device__ __forceinline__ void lds_add(float* p, float v) {
@@ -781,7 +794,7 @@ __device__ __forceinline__ void edge_shift(const Net& net, const BlockW& bw, con
     sh[d] = (phx * r[d]) / den;
     sh[D + d] = NT ? (phxT * r[d] + phx * dr[d]) / den - (phx * r[d]) * dlength / (den * den) : 0.f;
   }
-  sc.sum_many<2 * D>(sh);
+  sc.sum_many<2 * D, true>(sh);
   if (writer && kk == 0) {
 #pragma unroll
     for (int d = 0; d < D; ++d) {
@@ -832,7 +845,7 @@ __device__ __forceinline__ void edge_tail(const Net& net, const BlockW& bw, cons
 #pragma unroll
     for (int r16 = 0; r16 < 16; ++r16) v[r16] = m[fb][r16] * g;
 #ifndef ECNF_EXP_NO_AGG
-    sc.sum_many<16>(v);
+    sc.sum_many<16, true>(v);
 #endif
     if (writer) {
       if (agg_dst) {
@@ -849,7 +862,7 @@ __device__ __forceinline__ void edge_tail(const Net& net, const BlockW& bw, cons
     if constexpr (NT) {
 #pragma unroll
       for (int r16 = 0; r16 < 16; ++r16) v[r16] = gT * m[fb][r16] + g * mT[fb][r16];
-      sc.sum_many<16>(v);
+      sc.sum_many<16, true>(v);
       if (writer) {
 #pragma unroll
         for (int r16 = 0; r16 < 16; ++r16)

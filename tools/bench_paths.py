@@ -2,7 +2,7 @@
 
 Each line: config, batch, solver, divergence, ms per launch (median of REPS HIP-event timings on the launch stream),
 molecules/s, mean NFE per molecule, and achieved algorithmic TFLOP/s counting (1 + tangents) x F per evaluation
-(F = bench.flops_per_eval; Hutchinson = 1 tangent, exact = N*D tangents).  Synthetic seeded inputs, flax-default
+(F = bench.live_flops_per_eval; Hutchinson = 1 tangent, exact = N*D tangents).  Synthetic seeded inputs, flax-default
 random-init weights.  Usage: [ECNF_PATHS_ONLY=qm9,aldp] python tools/bench_paths.py [out.json]
 """
 import json
@@ -16,7 +16,7 @@ sys.path.insert(0, ROOT)
 
 import torch  # noqa: E402
 
-from bench import flops_per_eval  # noqa: E402
+from bench import live_flops_per_eval  # noqa: E402
 from ecnf_amd import CONFIGS, init_params, _lib  # noqa: E402
 from ecnf_amd.engine import EcnfHandle, SolveOptions  # noqa: E402
 
@@ -61,7 +61,7 @@ def run_case(name, B, solver, step, div, direction):
     ms = sorted(ts)[len(ts) // 2]
     nfe_mean = float(nfe.float().mean())
     tangents = {"none": 0, "hutchinson": 1, "exact": cfg.event_dim}[div]
-    flop = B * nfe_mean * flops_per_eval(cfg) * (1 + tangents)
+    flop = B * nfe_mean * live_flops_per_eval(cfg) * (1 + tangents)
     rec = {"config": name, "batch": B, "solver": solver, "step": step, "divergence": div, "direction": direction,
            "ms": round(ms, 3), "molecules_per_s": round(B / ms * 1e3, 1), "nfe_mean": round(nfe_mean, 2),
            "tflops": round(flop / ms / 1e9, 2), "bad_status": int((st != 0).sum()),
