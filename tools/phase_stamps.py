@@ -18,6 +18,7 @@ NAMES = ["prologue", "node_dense", "p_gemm", "edge", "node_update", "phi_h", "ep
          "edge_phix_chain(w0)"]
 name = sys.argv[1] if len(sys.argv) > 1 else "lj13"
 B = int(sys.argv[2]) if len(sys.argv) > 2 else 1024
+DIV = sys.argv[3] if len(sys.argv) > 3 else "none"   # none | hutchinson (the tangent kernel)
 cfg = CONFIGS[name]
 h = EcnfHandle(cfg, init_params(cfg, 0), 0)
 lib = h.lib
@@ -25,12 +26,14 @@ lib.ecnf_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
 z = torch.randn((B, cfg.event_dim), device="cuda")
 x0 = h.base_sample(z)
 feat = torch.zeros((B, cfg.n_nodes), device="cuda", dtype=torch.int32)
-h.integrate(x0, feat, 0.0, 1.0, SolveOptions("euler", 0.01))
+eps = torch.randn((B, cfg.event_dim), device="cuda") if DIV == "hutchinson" else None
+div = _lib.DIV_HUTCHINSON if DIV == "hutchinson" else _lib.DIV_NONE
+h.integrate(x0, feat, 0.0, 1.0, SolveOptions("euler", 0.01), div, eps)
 buf = (ctypes.c_ulonglong * 32)()
 lib.ecnf_debug_stamps(buf, 32, 1)
 ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 ev0.record()
-h.integrate(x0, feat, 0.0, 1.0, SolveOptions("euler", 0.01))
+h.integrate(x0, feat, 0.0, 1.0, SolveOptions("euler", 0.01), div, eps)
 ev1.record()
 torch.cuda.synchronize()
 lib.ecnf_debug_stamps(buf, 32, 1)
@@ -38,7 +41,7 @@ nwg = buf[28]
 cyc = [buf[i] / nwg for i in range(len(NAMES))]
 tot = sum(cyc[:8])
 real_us = buf[29] / nwg / 100.0   # s_memrealtime is 100 MHz
-out = {"config": name, "batch": B, "workgroups": nwg, "kernel_ms": ev0.elapsed_time(ev1),
+out = {"config": name, "batch": B, "divergence": DIV, "workgroups": nwg, "kernel_ms": ev0.elapsed_time(ev1),
        "cycles_per_wg": tot, "wg_wall_us": real_us, "clock_GHz": tot / (real_us * 1e3),
        "shares": {n: cyc[i] / tot for i, n in enumerate(NAMES[:8])},
        "edge_wave0_shares_of_edge": {n: cyc[i] / max(cyc[3], 1) for i, n in list(enumerate(NAMES))[8:]}}
