@@ -184,6 +184,9 @@ struct ChainInv {
   float v[2 * 4 - 1];
 };
 
+#ifndef ECNF_CHAIN_PRIO
+#define ECNF_CHAIN_PRIO 1   // wave priority inside chain_split (s_setprio)
+#endif
 #ifndef ECNF_SPLIT_PF
 #define ECNF_SPLIT_PF 3
 #endif
@@ -218,6 +221,8 @@ __device__ __forceinline__ void chain_split(SplitX<NF>& XA, SplitX<NF>& XB, f32x
                                             const ChainInv& inv, int lane, SplitX<NF>& XAT, SplitX<NF>& XBT,
                                             f32x16 (&accT)[NF]) {
   using Plan = SplitPlan<NF, NL>;
+  // the chain wave issues first on its SIMD while its partner wave is in VALU / LDS work (A/B: 26.14 -> 25.99 ms)
+  __builtin_amdgcn_s_setprio(ECNF_CHAIN_PRIO);
   constexpr int GB = Plan::GB, GL = Plan::GL, G = Plan::G, NI = Plan::NI, PF = ECNF_SPLIT_PF;
   constexpr int GE = Plan::last_group() + 1;   // groups including the VALU-only tail
   const int kk = lane >> 5;
@@ -398,6 +403,7 @@ __device__ __forceinline__ void chain_split(SplitX<NF>& XA, SplitX<NF>& XB, f32x
       __builtin_amdgcn_sched_barrier(0);
     }
   });
+  __builtin_amdgcn_s_setprio(0);
 }
 
 // primal-only chain (the tangent arguments alias the primal ones and are never touched)
