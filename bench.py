@@ -1,24 +1,33 @@
 """bench.py — sampled molecules/sec for the equivariant-CNF sample path (BASELINE.json `metric`).
 
-Workload (BASELINE.json configs[1]): LJ13 (N = 13, D = 3, lj13.yaml network), batch 1024 molecules per GPU,
-fixed-step ODE with NFE = 100 (Euler, dt = 0.01), fp32, synthetic inputs (x0 from the zero-CoM
-base with a seeded draw) and flax-default random-init weights of the lj13 architecture.
+Workloads (BASELINE.json configs):
+  * N = 1 (configs[1], the headline): LJ13 (N = 13, D = 3, lj13.yaml network), batch 1024, fixed-step ODE with
+    NFE = 100 (Euler, dt = 0.01), synthetic inputs (x0 from the zero-CoM base with a seeded
+    draw) and flax-default random-init weights of the lj13 architecture.
+  * N > 1 (configs[4]): LJ13 global batch 65536 sharded contiguously over the N ranks (65536 / N molecules per GPU,
+    one process per GPU, RCCL), plus the eval leg of setup_training.py:166-185: sample_and_log_prob_cnf (Hutchinson,
+    Euler NFE = 100) -> LJ13 target log-density -> log_w -> reverse / forward ESS, reduced over RCCL (one MAX and one
+    SUM all-reduce).  Noise is one seeded global draw, so every molecule's result is independent of N.
 
-One "step" = one full sample of the batch: x0 (resident in HBM) -> 100 EGNN evaluations -> x1, i.e. one
-ecnf_integrate launch.  Multi-GPU: one process per GPU (torchrun), each rank samples its own 1024 molecules
-(weak scaling, no data-path collective); the timing is the max over ranks.
+One "step" = one full sample of the rank's shard: x0 (resident in HBM) -> 100 EGNN evaluations -> x1, i.e. one
+ecnf_integrate launch.  The timing is the max over ranks, bracketed by barriers and device syncs.
+
+Launch: `python bench.py --gpus N` with WORLD_SIZE unset starts the N rank processes itself (torch.distributed.run as a
+CHILD process, before this process touches the GPU) and exits with its status; under torchrun it is one rank.
 
 Extra fields: "roofline" (dominant kernel = integrate_kernel, MFMA bound: algorithmic fp32 FLOPs per launch /
 average launch time from HIP events on the launch stream, against the ceiling of the kernel's instruction mix —
-GEMM FLOPs at the split-fp16 rate, vector FLOPs at the fp32 rate; see roofline_peak), "matmul" (which
-arithmetic the GEMMs run) and "cpu_baseline" (the oracle's numpy fp32 batched
-restatement of the same Euler solve on a bounded sample, rank 0 at N = 1 only).
+GEMM FLOPs at the split-fp16 rate, vector FLOPs at the fp32 rate; see roofline_peak), "matmul" (which arithmetic the
+GEMMs run, and the strict-fp32 kernels' time on the same workload), "logprob" (the eval leg) and "cpu_baseline" (a
+torch-CPU fp32 batched restatement of the same Euler solve on a bounded sample, rank 0 at N = 1 only).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -29,6 +38,7 @@ sys.path.insert(0, ROOT)
 PEAK_FP32_MFMA_TFLOPS = 157.3    # MI355X dense FP32 matrix peak (MI355X_MICROARCH.md, chip-level parameters)
 PEAK_16BIT_MFMA_TFLOPS = 2516.6  # MI355X dense BF16 = FP16 matrix peak: 256 CU x 4 SIMD x 1024 FLOP/clk x 2.4 GHz
 SPLIT_TERMS = {"split_f16": 3, "split_bf16": 6}   # 16-bit cross terms per fp32 product (chain_split.hpp)
+GLOBAL_BATCH_MULTI = 65536       # BASELINE.json configs[4]
 
 
 def flops_per_eval(cfg) -> float:
@@ -74,23 +84,60 @@ def roofline_peak(cfg, chain_mode: str) -> float:
     return F / ((F - Fv) / p_split + Fv / PEAK_FP32_MFMA_TFLOPS)
 
 
-def cpu_baseline(cfg_name: str, n_mol: int, nfe: int, threads: int):
-    """Time the oracle (numpy fp32, batched like XLA's vmap) on `n_mol` molecules x `nfe` Euler steps."""
+def cpu_model() -> str:
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=20).stdout
+        for line in out.splitlines():
+            if line.startswith("Model name:"):
+                return line.split(":", 1)[1].strip()
+    except Exception:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(cfg_name: str, n_mol: int, n_mol_1t: int, nfe: int, threads: int):
+    """The torch-CPU fp32 batched restatement (oracle/torch_ref.py, the batched-GEMM structure XLA builds from
+    vmap) of the same Euler NFE-step sample, timed on `n_mol` molecules with `threads` threads and on `n_mol_1t`
+    molecules with one thread.  Returns (rate_all, secs_all, rate_1t, secs_1t)."""
     import numpy as np
-    from threadpoolctl import threadpool_limits
+    import torch
     from oracle import ecnf_oracle as O
+    from oracle import torch_ref as R
     oc = O.CONFIGS[cfg_name]
-    params = O.init_params(oc, 0)
+    P = R.to_torch(O.init_params(oc, 0))
     rng = np.random.default_rng(0)
-    z = rng.standard_normal((n_mol, oc.n_nodes * oc.dim)).astype(np.float32)
-    x0 = O.base_sample(z, oc)
-    feat = np.zeros((n_mol, oc.n_nodes), np.int32)
-    with threadpool_limits(limits=threads):
-        O.sample_cnf(params, oc, x0[:2], feat[:2], solver="euler", dt0=0.5)   # warm-up
-        t0 = time.perf_counter()
-        O.sample_cnf(params, oc, x0, feat, solver="euler", dt0=1.0 / nfe)
-        dt = time.perf_counter() - t0
-    return n_mol / dt, dt
+    z = rng.standard_normal((max(n_mol, n_mol_1t), oc.n_nodes * oc.dim)).astype(np.float32)
+    x0 = torch.from_numpy(O.base_sample(z, oc))
+    feat = torch.zeros((x0.shape[0], oc.n_nodes), dtype=torch.int32)
+    prev = torch.get_num_threads()
+    out = []
+    try:
+        for th, n in ((threads, n_mol), (1, n_mol_1t)):
+            torch.set_num_threads(th)
+            R.sample_euler(P, oc, x0[:2], feat[:2], 2)     # warm-up
+            t0 = time.perf_counter()
+            R.sample_euler(P, oc, x0[:n], feat[:n], nfe)
+            dt = time.perf_counter() - t0
+            out += [n / dt, dt]
+    finally:
+        torch.set_num_threads(prev)
+    return tuple(out)
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int) -> int:
+    """Start n rank processes of this script under torch.distributed.run as a CHILD (this process has not touched
+    the GPU) and return its exit status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
 
 
 def main():
@@ -98,40 +145,57 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--batch", type=int, default=1024, help="molecules per GPU per step")
+    ap.add_argument("--batch", type=int, default=0,
+                    help="GLOBAL molecules per step (default: 1024 at one rank, 65536 over several ranks)")
     ap.add_argument("--config", default="lj13")
     ap.add_argument("--nfe", type=int, default=100)
-    ap.add_argument("--cpu-molecules", type=int, default=160, help="bounded CPU-baseline sample (0 = skip)")
+    ap.add_argument("--logprob", type=int, default=-1,
+                    help="eval leg (sample + Hutchinson log-prob + target + ESS) passes: default 1 over several ranks, "
+                         "0 at one rank")
+    ap.add_argument("--fp32-steps", type=int, default=2, help="launches of the strict-fp32 kernels timed (0 = skip)")
+    ap.add_argument("--cpu-molecules", type=int, default=256, help="bounded CPU-baseline sample (0 = skip)")
+    ap.add_argument("--cpu-molecules-1t", type=int, default=48, help="bounded 1-thread CPU-baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "0") or 0))
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL over xGMI) or gloo (multi-rank rehearsal)")
+    ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--dump", default="", help="directory: each rank saves its shard's outputs (tests)")
     args = ap.parse_args()
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
 
     import numpy as np
     import torch
     import torch.distributed as dist
     from ecnf_amd import CONFIGS, init_params
+    from ecnf_amd import _lib
+    from ecnf_amd import distributed as D
     from ecnf_amd.engine import EcnfHandle, SolveOptions
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    ndev = max(1, torch.cuda.device_count())
-    local = local % ndev                      # one rank per GPU; folds ranks onto fewer GPUs only in rehearsals
     if world > 1:
+        ndev = max(1, torch.cuda.device_count())
+        local = local % ndev                  # one rank per GPU; folds ranks onto fewer GPUs only in rehearsals
         torch.cuda.set_device(local)
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(args.dist_backend)
+        world = dist.get_world_size()         # the world the process group actually formed
+        rank = dist.get_rank()
     dev = torch.device("cuda", local)
     cfg = CONFIGS[args.config]
+    G = args.batch or (GLOBAL_BATCH_MULTI if world > 1 else 1024)
+    lo, hi = D.shard_bounds(G, rank, world)
+    B = hi - lo
+    n_logprob = args.logprob if args.logprob >= 0 else (1 if world > 1 else 0)
 
     h = EcnfHandle(cfg, init_params(cfg, 0), local)
-    g = torch.Generator(device=dev)
-    g.manual_seed(1234 + rank)                       # each rank samples its own molecules
-    z = torch.randn((args.batch, cfg.event_dim), generator=g, device=dev)
+    z = D.global_normal(G, cfg.event_dim, args.seed, lo, hi, dev)     # rows [lo, hi) of one global draw
     x0 = h.base_sample(z)
-    feat = torch.zeros((args.batch, cfg.n_nodes), device=dev, dtype=torch.int32)
+    feat = torch.zeros((B, cfg.n_nodes), device=dev, dtype=torch.int32)
     opts = SolveOptions(solver="euler", step_size=1.0 / args.nfe)
 
     def step():
@@ -140,12 +204,22 @@ def main():
     for _ in range(args.warmup):
         y1, _, nfe, _ = step()
     torch.cuda.synchronize(dev)
-    nfe_seen = int(nfe.max()) if args.warmup else args.nfe
+    nfe_seen = int(nfe.max()) if args.warmup and B else args.nfe
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    def max_over_ranks(x: float) -> float:
+        if world == 1:
+            return x
+        t = torch.tensor([x], device=dev if args.dist_backend == "nccl" else "cpu", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
 
     stream = torch.cuda.current_stream(dev)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    if world > 1:
-        dist.barrier()
+    barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for i in range(args.steps):
@@ -153,35 +227,74 @@ def main():
         y1, _, nfe, status = step()
         ev[i][1].record(stream)
     torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed], device=dev if args.dist_backend == "nccl" else "cpu", dtype=torch.float64)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    t_max = float(t.item())
-    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    barrier()
+    t_max = max_over_ranks(time.perf_counter() - t0)
+    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev])) if args.steps else 0.0
     assert int((status != 0).sum()) == 0 and torch.isfinite(y1).all()
 
-    value = world * args.batch * args.steps / t_max
+    value = G * args.steps / t_max
     F = live_flops_per_eval(cfg)
-    achieved = F * nfe_seen * args.batch / (kernel_ms * 1e-3) / 1e12
+    achieved = F * nfe_seen * B / (kernel_ms * 1e-3) / 1e12
     chain_mode = h.chain_arithmetic()
     peak = roofline_peak(cfg, chain_mode)
 
-    traffic = None
-    pmc = os.path.join(ROOT, "profiles", f"pmc_traffic_{args.config}_b{args.batch}.json")
-    if os.path.exists(pmc):
-        with open(pmc) as f:
-            traffic = json.load(f).get("hbm_bytes_per_launch")
+    # the strict-fp32 kernels (every GEMM on v_mfma_f32_32x32x2_f32) on the same workload, for comparison
+    fp32 = None
+    if args.fp32_steps > 0 and B:
+        h.set_precision("fp32")
+        y1_32, _, _, _ = step()
+        torch.cuda.synchronize(dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(args.fp32_steps):
+            y1_32, _, _, _ = step()
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        h.set_precision("split_f16")
+        ms32 = e0.elapsed_time(e1) / args.fp32_steps
+        fp32 = {"kernel_ms": ms32, "molecules_per_s_per_gpu": B / (ms32 * 1e-3),
+                "achieved_tflops": F * nfe_seen * B / (ms32 * 1e-3) / 1e12,
+                "max_abs_diff_vs_split": float((y1_32 - y1).abs().max())}
+
+    # eval leg (setup_training.py:166-185): sample_and_log_prob_cnf(approx=True) -> target -> log_w -> ESS
+    logprob = None
+    if n_logprob > 0:
+        from ecnf_amd import targets as T
+        for i in range(n_logprob + 1):        # pass 0 warms up
+            barrier()
+            torch.cuda.synchronize(dev)
+            t1 = time.perf_counter()
+            x1, dl, _, st = h.integrate(x0, feat, 0.0, 1.0, opts, divergence=_lib.DIV_HUTCHINSON, eps=z,
+                                        check_status=False)
+            log_q = h.base_log_prob(x0) - dl          # sample_and_log_prob.py:147 (eps = z: the ref's quirk)
+            log_p = T.lj_log_prob(x1, cfg.n_nodes, cfg.dim) if args.config == "lj13" else \
+                T.dw_log_prob(x1, cfg.n_nodes, cfg.dim)
+            log_w = log_p - log_q
+            fwd, rev = D.ess_from_device(log_w)       # RCCL: one MAX + one SUM all-reduce
+            mean_lq = D.masked_mean(log_q)
+            torch.cuda.synchronize(dev)
+            barrier()
+            t_lp = max_over_ranks(time.perf_counter() - t1)
+        logprob = {"workload": f"{args.config} sample_and_log_prob_cnf (Hutchinson, Euler NFE={args.nfe}) + target "
+                               f"log-density + ESS over {'RCCL' if args.dist_backend == 'nccl' else args.dist_backend}",
+                   "molecules_per_s": G / t_lp, "ms": t_lp * 1e3, "rev_ess": float(rev), "fwd_ess": float(fwd),
+                   "mean_log_q": float(mean_lq), "status_ok": bool(int((st != 0).sum()) == 0)}
+        if args.dump:
+            os.makedirs(args.dump, exist_ok=True)
+            np.savez(os.path.join(args.dump, f"rank{rank}.npz"), lo=lo, hi=hi, x1=y1.cpu().numpy(),
+                     x1_lp=x1.cpu().numpy(), log_q=log_q.cpu().numpy(), log_w=log_w.cpu().numpy(),
+                     rev_ess=float(rev), fwd_ess=float(fwd), mean_log_q=float(mean_lq), world=world)
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_molecules > 0:
         threads = args.cpu_threads or len(os.sched_getaffinity(0))
-        rate, secs = cpu_baseline(args.config, args.cpu_molecules, args.nfe, threads)
-        cpu = {"value": rate, "unit": "molecules/s", "cores": threads, "kind": "port",
-               "sample": f"{args.cpu_molecules} LJ13 molecules x {args.nfe} Euler steps, oracle numpy fp32 "
-                         f"batched restatement ({secs:.1f} s)"}
+        r_all, s_all, r_1, s_1 = cpu_baseline(args.config, args.cpu_molecules, args.cpu_molecules_1t, args.nfe,
+                                              threads)
+        cpu = {"value": r_all, "unit": "molecules/s", "cores": threads, "kind": "port",
+               "value_1_thread": r_1, "cpu_model": cpu_model(),
+               "sample": f"{args.cpu_molecules} {args.config} molecules x {args.nfe} Euler steps on {threads} threads "
+                         f"({s_all:.1f} s) and {args.cpu_molecules_1t} on 1 thread ({s_1:.1f} s); torch-CPU fp32 "
+                         f"batched restatement (oracle/torch_ref.py)"}
 
     if rank == 0:
         out = {
@@ -191,29 +304,36 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": t_max / args.steps * 1e3,
+            "ms_per_step": t_max / args.steps * 1e3 if args.steps else 0.0,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if world > 1 and not args.batch else "weak",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": "f32 (split_f16x3: fp32 operands as two fp16 pieces, 3 cross terms, fp32 accumulate)"
+                     if chain_mode == "split_f16" else "f32",
             "data": "synthetic (seeded zero-CoM Gaussian x0, flax-default random-init lj13 weights)",
-            "config": {"workload": f"{args.config} sample, Euler NFE={nfe_seen}, batch {args.batch}/GPU",
-                       "n_nodes": cfg.n_nodes, "batch_per_gpu": args.batch, "global_batch": world * args.batch,
+            "config": {"workload": f"{args.config} sample, Euler NFE={nfe_seen}, global batch {G} "
+                                   f"({B} per GPU on rank 0)",
+                       "n_nodes": cfg.n_nodes, "batch_per_gpu": B, "global_batch": G,
                        "nfe": nfe_seen, "solver": "euler", "parallelism": f"dp{world}"},
-            "matmul": {"gemms": chain_mode, "tangent_kernels": f"{chain_mode} edge chains, fp32_mfma node GEMMs",
-                       "accumulate": "f32"},
+            "matmul": {"gemms": chain_mode, "tangent_kernels": h.chain_arithmetic(True) + " edge chains",
+                       "accumulate": "f32", "strict_fp32": fp32},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
-                         "frac": achieved / peak, "traffic": traffic,
+                         "frac": achieved / peak, "traffic": None,
                          "kernel": "integrate_kernel", "kernel_ms": kernel_ms,
-                         "flop_per_launch": F * nfe_seen * args.batch,
+                         "flop_per_launch": F * nfe_seen * B,
                          "flop_basis": "live dense-contraction FLOPs per EGNN eval (SURVEY 8d F minus the last "
                                        "block's dead h update) x NFE x batch",
                          "frac_vs_fp32_mfma_peak": achieved / PEAK_FP32_MFMA_TFLOPS,
                          "peak_basis": (f"GEMM FLOPs at the dense 16-bit MFMA peak / {SPLIT_TERMS[chain_mode]} split "
                                         "terms, vector FLOPs at the fp32 peak") if chain_mode in SPLIT_TERMS
                                        else "fp32 MFMA peak"},
+            "logprob": logprob,
             "cpu_baseline": cpu,
         }
+        pmc = os.path.join(ROOT, "profiles", f"pmc_traffic_{args.config}_b{B}.json")
+        if os.path.exists(pmc):
+            with open(pmc) as f:
+                out["roofline"]["traffic"] = json.load(f).get("hbm_bytes_per_launch")
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -21,8 +21,11 @@
 
 namespace ecnf {
 
-#define ECNF_INST_PRIMAL(m, l, d) ECNF_INST_SHAPE(ECNF_INST_KW, m, l, d, 0)
-#define ECNF_INST_BOTH(m, l, d) ECNF_INST_SHAPE(ECNF_INST_KW, m, l, d, 0) ECNF_INST_SHAPE(ECNF_INST_KW, m, l, d, 1)
+// every shape in both GEMM arithmetics (P = 0 split fp16, P = 1 strict fp32)
+#define ECNF_INST_PRIMAL(m, l, d) \
+  ECNF_INST_SHAPE(ECNF_INST_KW, m, l, d, 0, 0) ECNF_INST_SHAPE(ECNF_INST_KW, m, l, d, 0, 1)
+#define ECNF_INST_BOTH(m, l, d) \
+  ECNF_INST_PRIMAL(m, l, d) ECNF_INST_SHAPE(ECNF_INST_KW, m, l, d, 1, 0) ECNF_INST_SHAPE(ECNF_INST_KW, m, l, d, 1, 1)
 #ifdef ECNF_SPLIT_TU
 #define ECNF_INST_KW extern template
 #else
@@ -67,7 +70,8 @@ __global__ void base_log_prob_kernel(const float* __restrict__ y, float* out, in
 }
 
 // -log_p = energy of the LJ / DW targets (leonard_jones.py:10-27, double_well.py:9-19), one thread per molecule.
-// The reference sums f(d) over the N(N-1) ordered pairs; each unordered pair is visited once here and counted twice.
+// The reference sums f(d) over the N(N-1) ordered pairs; each unordered pair is visited once here and both orders
+// are added (LJ: with the receiver's r, a per-node array when r_nodes != NULL).
 __global__ void target_log_prob_kernel(ecnf_target t, const float* __restrict__ x, float* log_p, int B) {
   const int bb = blockIdx.x * blockDim.x + threadIdx.x;
   if (bb >= B) return;
@@ -82,15 +86,16 @@ __global__ void target_log_prob_kernel(ecnf_target t, const float* __restrict__ 
         x2 += v * v;
       }
       const float dist = sqrtf(x2 == 0.f ? 1.0f : x2);   // safe_norm (numerical.py:7-10)
-      float f;
       if (t.kind == ECNF_TARGET_LJ) {
-        const float q = t.r / dist, q2 = q * q, q6 = q2 * q2 * q2;
-        f = q6 * q6 - 2.0f * q6;
+        // ordered pairs (receiver i, sender j) and (j, i) use the receiver's r (leonard_jones.py:20)
+        const float ri = t.r_nodes ? t.r_nodes[i] : t.r, rj = t.r_nodes ? t.r_nodes[j] : t.r;
+        const float qi = ri / dist, qi2 = qi * qi, qi6 = qi2 * qi2 * qi2;
+        const float qj = rj / dist, qj2 = qj * qj, qj6 = qj2 * qj2 * qj2;
+        pair += (qi6 * qi6 - 2.0f * qi6) + (qj6 * qj6 - 2.0f * qj6);
       } else {
         const float u = dist - t.d0, u2 = u * u;
-        f = t.a * u + t.b * u2 + t.c * u2 * u2;
+        pair += 2.0f * (t.a * u + t.b * u2 + t.c * u2 * u2);
       }
-      pair += 2.0f * f;
     }
   float e;
   if (t.kind == ECNF_TARGET_LJ) {
@@ -114,20 +119,26 @@ __global__ void target_log_prob_kernel(ecnf_target t, const float* __restrict__ 
 // log-sum-exp partials (max, sum exp(s v - max)) for s = +1, -1, +2 and the count, one workgroup: online
 // rescaling per thread, then a tree over the workgroup in LDS
 constexpr int kLseThreads = 1024;
+// v = -inf has zero weight (exp(-inf) = 0, as jax.nn.logsumexp gives it) and is skipped; equal maxima (+inf) add
+// their counts instead of exp(inf - inf) = NaN.  A NaN value makes the partial NaN.
 __device__ __forceinline__ void lse_push(float& m, float& s, float v) {
+  if (v == -INFINITY) return;
   if (v > m) {
-    s = s * __expf(m - v) + 1.0f;
+    s = (m == -INFINITY ? 0.0f : s * __expf(m - v)) + 1.0f;
     m = v;
   } else {
-    s += __expf(v - m);
+    s += (v == m) ? 1.0f : __expf(v - m);
   }
 }
 __device__ __forceinline__ void lse_merge(float& m, float& s, float m2, float s2) {
   if (m2 > m) {
-    s = s * __expf(m - m2) + s2;
+    s = (m == -INFINITY ? 0.0f : s * __expf(m - m2)) + s2;
     m = m2;
   } else if (m2 > -INFINITY) {
-    s += s2 * __expf(m2 - m);
+    s += (m2 == m) ? s2 : s2 * __expf(m2 - m);
+  } else if (m2 != m2) {
+    m = m2;
+    s = m2;
   }
 }
 __global__ __launch_bounds__(kLseThreads) void lse_partials_kernel(const float* __restrict__ v,
@@ -217,8 +228,9 @@ struct ecnf_handle {
   ecnf_cfg cfg;
   int device;
   float* dbuf;
-  Net net[2];          // [NT]
-  size_t lds[2];       // dynamic LDS bytes per workgroup [NT]
+  int prec;            // ecnf_precision of later calls
+  Net net[4];          // [2 P + NT]
+  size_t lds[4];       // dynamic LDS bytes per workgroup [2 P + NT]
 };
 
 namespace {
@@ -328,7 +340,12 @@ struct HostBlock {
   const float *nb, *nk;
 };
 
-int choose_mpw(const ecnf_cfg& c, int NT, int* mpw_out, size_t* lds_out, int* rp_out) {
+// Geo<NF, NT, P>::kSplit: the split primal kernels (16-B node-row strides, stored segment parts)
+bool split_primal(const ecnf_cfg& c, int NT, int P) {
+  return kSplitChain && P == 0 && !NT && c.mlp_width <= 32 * kSplitMaxNF;
+}
+
+int choose_mpw(const ecnf_cfg& c, int NT, int P, int* mpw_out, size_t* lds_out, int* rp_out) {
   const int N = c.n_nodes, D = c.dim, H = c.hidden, T = c.time_embedding_dim, M = c.mlp_width;
   const int E = N * (N - 1);
   const char* env = std::getenv(NT ? "ECNF_MPW_TANGENT" : "ECNF_MPW");
@@ -339,7 +356,7 @@ int choose_mpw(const ecnf_cfg& c, int NT, int* mpw_out, size_t* lds_out, int* rp
   int best_rp = 0;
   for (int m = 1; m <= 32; ++m) {
     const int RP = 32 * ((m * N + 31) / 32);
-    const bool vec = kSplitChain && !NT && M <= 32 * kSplitMaxNF;   // Geo<NF, NT>::kSplit
+    const bool vec = split_primal(c, NT, P);
     const int floats = (NT ? lds_eval_floats<1>(N, D, H, T, M, m, RP, vec) : lds_eval_floats<0>(N, D, H, T, M, m, RP, vec)) +
                        solver_lds_floats(m, N * D);
     const size_t bytes = (size_t)floats * 4;
@@ -379,33 +396,37 @@ bool shape_supported(const ecnf_cfg& c, int NT) {
 hipError_t dispatch_integrate(const ecnf_handle* h, int NT, const SolveP& sp, const float* y0, const int32_t* feat,
                               const float* eps, float* y1, float* dlogp, int32_t* nfe, int32_t* status, int B,
                               hipStream_t stream) {
-  const int M = h->cfg.mlp_width, L = h->cfg.mlp_depth, D = h->cfg.dim;
-#define X(m, l, d)                                                                                        \
-  if (M == m && L == l && D == d)                                                                         \
-    return NT ? launch_integrate<m / 32, 1, l, d>(h->net[1], h->lds[1], sp, y0, feat, eps, y1, dlogp, nfe, status, B, stream) \
-              : launch_integrate<m / 32, 0, l, d>(h->net[0], h->lds[0], sp, y0, feat, eps, y1, dlogp, nfe, status, B, stream);
+  const int M = h->cfg.mlp_width, L = h->cfg.mlp_depth, D = h->cfg.dim, P = h->prec, ix = 2 * P + NT;
+#define ECNF_CALL(m, l, d, nt, p) \
+  launch_integrate<m / 32, nt, l, d, p>(h->net[ix], h->lds[ix], sp, y0, feat, eps, y1, dlogp, nfe, status, B, stream)
+#define X(m, l, d)                                                                                           \
+  if (M == m && L == l && D == d)                                                                            \
+    return NT ? (P ? ECNF_CALL(m, l, d, 1, 1) : ECNF_CALL(m, l, d, 1, 0)) : (P ? ECNF_CALL(m, l, d, 0, 1) : ECNF_CALL(m, l, d, 0, 0));
   ECNF_SHAPES(X)
 #undef X
 #define X(m, l, d) \
-  if (M == m && L == l && D == d && !NT) return launch_integrate<m / 32, 0, l, d>(h->net[0], h->lds[0], sp, y0, feat, eps, y1, dlogp, nfe, status, B, stream);
+  if (M == m && L == l && D == d && !NT) return P ? ECNF_CALL(m, l, d, 0, 1) : ECNF_CALL(m, l, d, 0, 0);
   ECNF_SHAPES_PRIMAL_ONLY(X)
 #undef X
+#undef ECNF_CALL
   return hipErrorInvalidValue;
 }
 
 hipError_t dispatch_vf(const ecnf_handle* h, int NT, const float* x, const float* t, const int32_t* feat,
                        const float* tan_in, int ntan, float* v, float* tan_out, int B, hipStream_t stream) {
-  const int M = h->cfg.mlp_width, L = h->cfg.mlp_depth, D = h->cfg.dim;
-#define X(m, l, d)                                                                           \
-  if (M == m && L == l && D == d)                                                            \
-    return NT ? launch_vf<m / 32, 1, l, d>(h->net[1], h->lds[1], x, t, feat, tan_in, ntan, v, tan_out, B, stream) \
-              : launch_vf<m / 32, 0, l, d>(h->net[0], h->lds[0], x, t, feat, tan_in, ntan, v, tan_out, B, stream);
+  const int M = h->cfg.mlp_width, L = h->cfg.mlp_depth, D = h->cfg.dim, P = h->prec, ix = 2 * P + NT;
+#define ECNF_CALL(m, l, d, nt, p) \
+  launch_vf<m / 32, nt, l, d, p>(h->net[ix], h->lds[ix], x, t, feat, tan_in, ntan, v, tan_out, B, stream)
+#define X(m, l, d)                                                                                           \
+  if (M == m && L == l && D == d)                                                                            \
+    return NT ? (P ? ECNF_CALL(m, l, d, 1, 1) : ECNF_CALL(m, l, d, 1, 0)) : (P ? ECNF_CALL(m, l, d, 0, 1) : ECNF_CALL(m, l, d, 0, 0));
   ECNF_SHAPES(X)
 #undef X
 #define X(m, l, d) \
-  if (M == m && L == l && D == d && !NT) return launch_vf<m / 32, 0, l, d>(h->net[0], h->lds[0], x, t, feat, tan_in, ntan, v, tan_out, B, stream);
+  if (M == m && L == l && D == d && !NT) return P ? ECNF_CALL(m, l, d, 0, 1) : ECNF_CALL(m, l, d, 0, 0);
   ECNF_SHAPES_PRIMAL_ONLY(X)
 #undef X
+#undef ECNF_CALL
   return hipErrorInvalidValue;
 }
 
@@ -602,8 +623,10 @@ int ecnf_create(const ecnf_cfg* cfg, const float* params, size_t n_floats, int d
   h->cfg = c;
   h->device = device;
   h->dbuf = dbuf;
-  for (int NT = 0; NT < 2; ++NT) {
-    Net& n = h->net[NT];
+  h->prec = ECNF_PREC_SPLIT_F16;
+  for (int ix = 0; ix < 4; ++ix) {
+    const int NT = ix & 1, P = ix >> 1;
+    Net& n = h->net[ix];
     std::memset(&n, 0, sizeof(Net));
     n.N = c.n_nodes; n.D = c.dim; n.H = H; n.T = T; n.M = M; n.L = L; n.K = K; n.nfeat = c.n_features;
     n.E = c.n_nodes * (c.n_nodes - 1);
@@ -638,11 +661,11 @@ int ecnf_create(const ecnf_cfg* cfg, const float* params, size_t n_floats, int d
     }
     int mpw = 0, rp = 0;
     size_t lds = 0;
-    if (shape_supported(c, NT) && choose_mpw(c, NT, &mpw, &lds, &rp) == ECNF_OK) {
+    if (shape_supported(c, NT) && choose_mpw(c, NT, P, &mpw, &lds, &rp) == ECNF_OK) {
       n.MPW = mpw;
       n.RP = rp;
       // split kernels store segment parts; the continuation rows [MPW][EP/32][ld_m] overlay hin (egnn_eval.hpp)
-      const bool vec = kSplitChain && !NT && M <= 32 * kSplitMaxNF;
+      const bool vec = split_primal(c, NT, P);
       n.cross = vec && (size_t)mpw * (n.EP / 32) * ld_node(M, 1, true) <= (size_t)rp * ld_node(H + T, 1, true) &&
                 n.EP / 32 <= kMaxTilesPerMol;
       // segments (receiver i: edges i(N-1) .. i(N-1)+N-2) that a tile boundary 32t splits; their continuation part
@@ -655,13 +678,13 @@ int ecnf_create(const ecnf_cfg* cfg, const float* params, size_t n_floats, int d
           n.xs_t[n.ncross] = (unsigned char)t;
           ++n.ncross;
         }
-      h->lds[NT] = lds;
+      h->lds[ix] = lds;
     } else {
       n.MPW = 0;
-      h->lds[NT] = 0;
+      h->lds[ix] = 0;
     }
   }
-  if (h->net[0].MPW == 0) {
+  if (h->net[0].MPW == 0 || h->net[2].MPW == 0) {
     hipFree(dbuf);
     delete h;
     return fail(ECNF_E_UNSUPPORTED, "configuration does not fit the LDS budget");
@@ -682,13 +705,27 @@ int ecnf_destroy(ecnf_handle* h) {
 
 int ecnf_molecules_per_workgroup(ecnf_handle* h, int32_t with_tangent, int32_t* mpw) {
   if (!h || !mpw) return fail(ECNF_E_INVALID, "NULL argument");
-  *mpw = h->net[with_tangent ? 1 : 0].MPW;
+  *mpw = h->net[2 * h->prec + (with_tangent ? 1 : 0)].MPW;
+  return ECNF_OK;
+}
+
+int ecnf_set_precision(ecnf_handle* h, int32_t precision) {
+  if (!h) return fail(ECNF_E_INVALID, "NULL handle");
+  if (precision != ECNF_PREC_SPLIT_F16 && precision != ECNF_PREC_FP32) return fail(ECNF_E_INVALID, "unknown precision");
+  h->prec = precision;
+  return ECNF_OK;
+}
+
+int ecnf_get_precision(ecnf_handle* h, int32_t* precision) {
+  if (!h || !precision) return fail(ECNF_E_INVALID, "NULL argument");
+  *precision = h->prec;
   return ECNF_OK;
 }
 
 int ecnf_chain_arithmetic(ecnf_handle* h, int32_t with_tangent, int32_t* mode) {
   if (!h || !mode) return fail(ECNF_E_INVALID, "NULL argument");
-  const bool split = kSplitChain && !with_tangent && h->cfg.mlp_width <= 32 * kSplitMaxNF;   // Geo<NF, NT>::kSplit
+  const bool split = split_primal(h->cfg, with_tangent ? 1 : 0, h->prec) ||
+                     (kSplitTanChain && h->prec == ECNF_PREC_SPLIT_F16 && with_tangent && h->cfg.mlp_width <= 128);
 #ifdef ECNF_SPLIT_BF16
   *mode = split ? ECNF_CHAIN_SPLIT_BF16 : ECNF_CHAIN_FP32_MFMA;
 #else
@@ -714,7 +751,7 @@ int ecnf_vf_jvp(ecnf_handle* h, const float* x, const float* t, const int32_t* f
   if (!h) return fail(ECNF_E_INVALID, "NULL handle");
   if (batch < 0 || n_tangents < 1) return fail(ECNF_E_INVALID, "batch < 0 or n_tangents < 1");
   if (batch > 0 && (!x || !t || !feat || !tan_in || !tan_out)) return fail(ECNF_E_INVALID, "NULL argument");
-  if (h->net[1].MPW == 0)
+  if (h->net[2 * h->prec + 1].MPW == 0)
     return fail(ECNF_E_UNSUPPORTED, "no tangent kernel for mlp_width=" + std::to_string(h->cfg.mlp_width));
   if (batch == 0) return ECNF_OK;
   HIP_TRY(hipSetDevice(h->device));
@@ -740,7 +777,7 @@ int ecnf_integrate(ecnf_handle* h, const ecnf_solve_opts* o, const float* y0, co
   if (adaptive && !(o->rtol > 0.f && o->atol > 0.f)) return fail(ECNF_E_INVALID, "adaptive stepping needs rtol, atol > 0");
   if (o->max_steps < 1) return fail(ECNF_E_INVALID, "max_steps < 1");
   const int NT = o->divergence == ECNF_DIV_NONE ? 0 : 1;
-  if (NT && h->net[1].MPW == 0)
+  if (NT && h->net[2 * h->prec + 1].MPW == 0)
     return fail(ECNF_E_UNSUPPORTED, "no tangent kernel for mlp_width=" + std::to_string(h->cfg.mlp_width));
   if (batch == 0) return ECNF_OK;
   SolveP sp;

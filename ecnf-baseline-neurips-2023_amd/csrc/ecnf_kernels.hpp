@@ -72,12 +72,23 @@ __device__ __forceinline__ float uniform_f(float x) {
 
 __device__ inline float clip_end(float tn, float tau1) { return tn > tau1 - 1e-6f ? tau1 : tn; }
 
+// embedding ids of one molecule (LDS [N]) in [0, n_features)?  Out-of-range ids are replaced by 0 (memory safety).
+__device__ inline bool check_features(const Net& net, int* f) {
+  bool ok = true;
+  for (int i = 0; i < net.N; ++i)
+    if (f[i] < 0 || f[i] >= net.nfeat) {
+      ok = false;
+      f[i] = 0;
+    }
+  return ok;
+}
+
 // one evaluation of the joint field g(tau, y) = dir * f(dir * tau, y) at (st.ts, st.ys) for every molecule
 // of the workgroup; writes kx_out [MPW][ND] and kl_out [MPW].  Exactly one egnn_eval call site (it is inlined).
-template <int NF, int NT, int L, int D>
+template <int NF, int NT, int L, int D, int P>
 __device__ __forceinline__ void joint_field(const Net& net, const Lds& s, const SolverLds& st, const SolveP& sp,
                                             float* kx_out, float* kl_out) {
-  constexpr int kThreads = Geo<NF, NT>::NTHR;
+  constexpr int kThreads = Geo<NF, NT, P>::NTHR;
   const int tid = opaque_tid(), MPW = net.MPW, ND = net.ND;
   // NT == 0: one primal eval; Hutchinson: one JVP along eps; exact: ND JVPs along e_k (trace of J)
   const int nrep = (NT == 0 || sp.div == ECNF_DIV_HUTCHINSON) ? 1 : ND;
@@ -91,7 +102,7 @@ __device__ __forceinline__ void joint_field(const Net& net, const Lds& s, const 
       }
       __syncthreads();
     }
-    egnn_eval<NF, NT, L, D>(net, s, st.ys, st.ts, st.tin, st.vout, st.tout);
+    egnn_eval<NF, NT, L, D, P>(net, s, st.ys, st.ts, st.tin, st.vout, st.tout);
     if constexpr (NT) {
       if (tid < MPW) {
         if (sp.div == ECNF_DIV_HUTCHINSON) {
@@ -121,16 +132,16 @@ __device__ inline float rms_state(float sumsq_x, float l, int ND, bool track) {
 enum Phase { kEuler = 0, kInit0 = 1, kInit1 = 2, kFsal = 3, kStage = 4 };
 
 // The whole solve as a phase machine around ONE field evaluation per loop trip.
-template <int NF, int NT, int L, int D>
-__global__ __launch_bounds__((Geo<NF, NT>::NTHR)) void integrate_kernel(Net net, SolveP sp, const float* __restrict__ y0,
+template <int NF, int NT, int L, int D, int P>
+__global__ __launch_bounds__((Geo<NF, NT, P>::NTHR)) void integrate_kernel(Net net, SolveP sp, const float* __restrict__ y0,
                                                                   const int32_t* __restrict__ feat,
                                                                   const float* __restrict__ eps, float* y1,
                                                                   float* dlogp, int32_t* nfe_out,
                                                                   int32_t* status_out, int B) {
-  constexpr int kThreads = Geo<NF, NT>::NTHR;
+  constexpr int kThreads = Geo<NF, NT, P>::NTHR;
   extern __shared__ float smem[];
   const int tid = threadIdx.x, MPW = net.MPW, ND = net.ND, N = net.N;
-  const Lds s = carve_lds<NT, Geo<NF, NT>::kSplit>(net, smem);
+  const Lds s = carve_lds<NT, Geo<NF, NT, P>::kSplit>(net, smem);
   const SolverLds st = carve_solver(s.tail, MPW, ND);
   const int mol0 = blockIdx.x * MPW;
   const int nmol = min(MPW, B - mol0);
@@ -157,6 +168,10 @@ __global__ __launch_bounds__((Geo<NF, NT>::NTHR)) void integrate_kernel(Net net,
     st.dt[tid] = sp.dt0;
     st.tnext[tid] = clip_end(fminf(sp.tau0 + sp.dt0, sp.tau1), sp.tau1);
   }
+  __syncthreads();
+  // device-side input check (no host sync on the call path): a molecule with an embedding id outside
+  // [0, n_features) reports ECNF_E_INVALID (nn.Embed would index out of range) and is solved with id 0
+  if (tid < nmol && !check_features(net, s.feat + tid * N)) st.status[tid] = ECNF_E_INVALID;
   __syncthreads();
 
   // Euler: ConstantStepSize, all molecules share the (uniform, register-held) time grid
@@ -218,7 +233,7 @@ __global__ __launch_bounds__((Geo<NF, NT>::NTHR)) void integrate_kernel(Net net,
     }
     __syncthreads();
 
-    joint_field<NF, NT, L, D>(net, s, st, sp, kx_out, kl_out);
+    joint_field<NF, NT, L, D, P>(net, s, st, sp, kx_out, kl_out);
 
     // ------------------------------------------------ consume it
     if (phase == kEuler) {
@@ -351,6 +366,13 @@ __global__ __launch_bounds__((Geo<NF, NT>::NTHR)) void integrate_kernel(Net net,
     atomicAdd(&g_stamps[28], 1ull);
   }
 #endif
+  // failure detection: a final state that is not finite (activations beyond the fp16 range of the split GEMMs, an
+  // overflowing field) is reported per molecule instead of passing as ECNF_OK
+  if (tid < nmol && st.status[tid] == ECNF_OK) {
+    bool fin = isfinite(st.lp[tid]);
+    for (int c = 0; c < ND; ++c) fin = fin && isfinite(st.y[tid * ND + c]);
+    if (!fin) st.status[tid] = ECNF_E_NONFINITE;
+  }
   for (int i = tid; i < nmol * ND; i += kThreads) y1[(size_t)mol0 * ND + i] = st.y[i];
   if (tid < nmol) {
     if (dlogp) dlogp[mol0 + tid] = st.lp[tid];
@@ -360,16 +382,16 @@ __global__ __launch_bounds__((Geo<NF, NT>::NTHR)) void integrate_kernel(Net net,
 }
 
 // one evaluation (and n_tangents JVPs) per molecule
-template <int NF, int NT, int L, int D>
-__global__ __launch_bounds__((Geo<NF, NT>::NTHR)) void vf_kernel(Net net, const float* __restrict__ x,
+template <int NF, int NT, int L, int D, int P>
+__global__ __launch_bounds__((Geo<NF, NT, P>::NTHR)) void vf_kernel(Net net, const float* __restrict__ x,
                                                            const float* __restrict__ t,
                                                            const int32_t* __restrict__ feat,
                                                            const float* __restrict__ tan_in, int ntan, float* v,
                                                            float* tan_out, int B) {
-  constexpr int kThreads = Geo<NF, NT>::NTHR;
+  constexpr int kThreads = Geo<NF, NT, P>::NTHR;
   extern __shared__ float smem[];
   const int tid = threadIdx.x, MPW = net.MPW, ND = net.ND, N = net.N;
-  const Lds s = carve_lds<NT, Geo<NF, NT>::kSplit>(net, smem);
+  const Lds s = carve_lds<NT, Geo<NF, NT, P>::kSplit>(net, smem);
   const SolverLds st = carve_solver(s.tail, MPW, ND);
   const int mol0 = blockIdx.x * MPW;
   const int nmol = min(MPW, B - mol0);
@@ -379,9 +401,13 @@ __global__ __launch_bounds__((Geo<NF, NT>::NTHR)) void vf_kernel(Net net, const 
   for (int i = tid; i < MPW * N; i += kThreads) s.feat[i] = (i / N) < nmol ? feat[(size_t)mol0 * N + i] : 0;
   if (tid < MPW) st.ts[tid] = tid < nmol ? t[mol0 + tid] : 0.f;
   __syncthreads();
+  // embedding ids outside [0, n_features): the molecule's outputs are NaN (no status output on this entry point)
+  if (tid < MPW) st.keep[tid] = (tid < nmol && !check_features(net, s.feat + tid * N)) ? 1 : 0;
+  __syncthreads();
+  const float kNaN = __builtin_nanf("");
   if constexpr (NT == 0) {
-    egnn_eval<NF, 0, L, D>(net, s, st.ys, st.ts, nullptr, st.vout, nullptr);
-    for (int i = tid; i < nmol * ND; i += kThreads) v[(size_t)mol0 * ND + i] = st.vout[i];
+    egnn_eval<NF, 0, L, D, P>(net, s, st.ys, st.ts, nullptr, st.vout, nullptr);
+    for (int i = tid; i < nmol * ND; i += kThreads) v[(size_t)mol0 * ND + i] = st.keep[i / ND] ? kNaN : st.vout[i];
   } else {
     for (int k = 0; k < ntan; ++k) {
       for (int i = tid; i < MPW * ND; i += kThreads) {
@@ -389,11 +415,11 @@ __global__ __launch_bounds__((Geo<NF, NT>::NTHR)) void vf_kernel(Net net, const 
         st.tin[i] = m < nmol ? tan_in[((size_t)(mol0 + m) * ntan + k) * ND + c] : 0.f;
       }
       __syncthreads();
-      egnn_eval<NF, 1, L, D>(net, s, st.ys, st.ts, st.tin, st.vout, st.tout);
+      egnn_eval<NF, 1, L, D, P>(net, s, st.ys, st.ts, st.tin, st.vout, st.tout);
       for (int i = tid; i < nmol * ND; i += kThreads) {
         const int m = i / ND, c = i - m * ND;
-        tan_out[((size_t)(mol0 + m) * ntan + k) * ND + c] = st.tout[i];
-        if (k == 0 && v) v[(size_t)mol0 * ND + i] = st.vout[i];
+        tan_out[((size_t)(mol0 + m) * ntan + k) * ND + c] = st.keep[m] ? kNaN : st.tout[i];
+        if (k == 0 && v) v[(size_t)mol0 * ND + i] = st.keep[m] ? kNaN : st.vout[i];
       }
       __syncthreads();
     }
@@ -401,27 +427,27 @@ __global__ __launch_bounds__((Geo<NF, NT>::NTHR)) void vf_kernel(Net net, const 
 }
 
 // ---- templated launchers (one instantiation per compiled shape and tangent flag) ----
-template <int NF, int NT, int L, int D>
+template <int NF, int NT, int L, int D, int P>
 hipError_t launch_integrate(const Net& net, size_t lds, const SolveP& sp, const float* y0, const int32_t* feat,
                             const float* eps, float* y1, float* dlogp, int32_t* nfe, int32_t* status, int B,
                             hipStream_t stream) {
-  auto k = integrate_kernel<NF, NT, L, D>;
+  auto k = integrate_kernel<NF, NT, L, D, P>;
   hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
   const int grid = (B + net.MPW - 1) / net.MPW;
-  hipLaunchKernelGGL(k, dim3(grid), dim3(Geo<NF, NT>::NTHR), lds, stream, net, sp, y0, feat, eps, y1, dlogp, nfe,
+  hipLaunchKernelGGL(k, dim3(grid), dim3(Geo<NF, NT, P>::NTHR), lds, stream, net, sp, y0, feat, eps, y1, dlogp, nfe,
                      status, B);
   return hipGetLastError();
 }
 
-template <int NF, int NT, int L, int D>
+template <int NF, int NT, int L, int D, int P>
 hipError_t launch_vf(const Net& net, size_t lds, const float* x, const float* t, const int32_t* feat,
                      const float* tan_in, int ntan, float* v, float* tan_out, int B, hipStream_t stream) {
-  auto k = vf_kernel<NF, NT, L, D>;
+  auto k = vf_kernel<NF, NT, L, D, P>;
   hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
   const int grid = (B + net.MPW - 1) / net.MPW;
-  hipLaunchKernelGGL(k, dim3(grid), dim3(Geo<NF, NT>::NTHR), lds, stream, net, x, t, feat, tan_in, ntan, v, tan_out,
+  hipLaunchKernelGGL(k, dim3(grid), dim3(Geo<NF, NT, P>::NTHR), lds, stream, net, x, t, feat, tan_in, ntan, v, tan_out,
                      B);
   return hipGetLastError();
 }
@@ -452,11 +478,11 @@ hipError_t launch_vf(const Net& net, size_t lds, const float* x, const float* t,
 
 
 // explicit instantiation (EXT = template) or instantiation declaration (EXT = extern template) of one shape
-#define ECNF_INST_SHAPE(EXT, m, l, d, NTV)                                                                    \
-  EXT hipError_t launch_integrate<m / 32, NTV, l, d>(const Net&, size_t, const SolveP&, const float*,         \
+#define ECNF_INST_SHAPE(EXT, m, l, d, NTV, PV)                                                                \
+  EXT hipError_t launch_integrate<m / 32, NTV, l, d, PV>(const Net&, size_t, const SolveP&, const float*,         \
                                                      const int32_t*, const float*, float*, float*, int32_t*, \
                                                      int32_t*, int, hipStream_t);                             \
-  EXT hipError_t launch_vf<m / 32, NTV, l, d>(const Net&, size_t, const float*, const float*, const int32_t*, \
+  EXT hipError_t launch_vf<m / 32, NTV, l, d, PV>(const Net&, size_t, const float*, const float*, const int32_t*, \
                                               const float*, int, float*, float*, int, hipStream_t);
 
 }  // namespace ecnf

@@ -52,11 +52,14 @@ constexpr bool kSplitTanChain = kSplitChain;
 #define ECNF_SPLIT_MAX_NF 8
 #endif
 constexpr int kSplitMaxNF = ECNF_SPLIT_MAX_NF;   // split chain up to M = 32 kSplitMaxNF
-template <int NF, int NT>
+// P: GEMM arithmetic of the kernel.  P = 0 (ECNF_PREC_SPLIT_F16, the default) as described above; P = 1
+// (ECNF_PREC_FP32, ecnf_set_precision) every GEMM on v_mfma_f32_32x32x2_f32 with fp32 operands: the strict-fp32
+// comparator and the fallback for molecules whose activations leave the fp16 range (ECNF_E_NONFINITE).
+template <int NF, int NT, int P = 0>
 struct Geo {
-  static constexpr bool kSplit = kSplitChain && NT == 0 && NF <= kSplitMaxNF;
+  static constexpr bool kSplit = kSplitChain && P == 0 && NT == 0 && NF <= kSplitMaxNF;
   // tangent kernels: the edge chains run split (chain_split_tangent); node GEMMs, layer 1 and the tail stay fp32
-  static constexpr bool kSplitT = kSplitTanChain && NT == 1 && NF <= 4;
+  static constexpr bool kSplitT = kSplitTanChain && P == 0 && NT == 1 && NF <= 4;
 #ifndef ECNF_SPLIT_NW
 #define ECNF_SPLIT_NW 8
 #endif
@@ -880,7 +883,7 @@ __device__ __forceinline__ void edge_tail(const Net& net, const BlockW& bw, cons
 }
 
 // one 32-edge tile through phi_e / gate / phi_x  (egnn.py:72-95)
-template <int NF, int NT, int L, int D>
+template <int NF, int NT, int L, int D, int P>
 __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, const Lds& s, int tile, int lane, bool agg) {
   const int kk = lane >> 5, li = lane & 31;
 #ifdef ECNF_EXP_CHAIN_ONLY
@@ -918,7 +921,7 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
   // split kernels: the row this lane's receiver-segment part is stored to — macc for the part in the tile where
   // the segment starts, the cross buffer (one row per molecule tile) for its continuation in the next tile
   float* agg_dst = nullptr;
-  if constexpr (Geo<NF, NT>::kSplit) {
+  if constexpr (Geo<NF, NT, P>::kSplit) {
     if (net.cross) {
       const int tloc = tile - mrow * (net.EP >> 5);
       agg_dst = tloc == ((i * nn1) >> 5) ? s.macc + rr * s.ld_m : s.cross + (mrow * (net.EP >> 5) + tloc) * s.ld_m;
@@ -954,7 +957,7 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
     for (int d = 0; d < D; ++d) dr[d] = 0.f;
   }
 
-  if constexpr (Geo<NF, NT>::kSplit) {
+  if constexpr (Geo<NF, NT, P>::kSplit) {
     // phi_e layer 1 from the per-node halves: pre = P_s[s] + P_r[r] + |r|^2 w_d  (egnn.py:76,79), SiLU, split
     SplitX<NF> XA, XB;
     f32x16 acc[NF];
@@ -1039,7 +1042,7 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
   STAMP_LANE0(s, kStEdgeLayer1, t_sub);
   // phi_e layers 2..L.  The weight pointer is laundered through an empty asm so the (tile-invariant) weight
   // loads are not hoisted out of the tile loop into thousands of live registers.
-  if constexpr (Geo<NF, NT>::kSplitT) {
+  if constexpr (Geo<NF, NT, P>::kSplitT) {
     // split-fp16 chains with tangents (chain_split_tangent; the staged chain biases are the log2-domain copies)
     ChainInv ie, ix;
     static_for<2 * 4 - 1>([&](auto Lc) {
@@ -1072,11 +1075,11 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
 // one full evaluation.  x_in/tan_in/v_out/tan_out: LDS [MPW][N*D]; t_in: LDS [MPW] (actual time).
 // Must be called by all 256 threads; returns after a barrier.
 // ---------------------------------------------------------------------------------------------------
-template <int NF, int NT, int L, int D>
+template <int NF, int NT, int L, int D, int P>
 __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const float* x_in, const float* t_in, const float* tan_in,
                           float* v_out, float* tan_out) {
-  constexpr int kNW = Geo<NF, NT>::NW, kNT = Geo<NF, NT>::NTHR;
-  constexpr bool kSplitG = Geo<NF, NT>::kSplit;
+  constexpr int kNW = Geo<NF, NT, P>::NW, kNT = Geo<NF, NT, P>::NTHR;
+  constexpr bool kSplitG = Geo<NF, NT, P>::kSplit;
   const int tid = opaque_tid(), lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: task indices stay in SGPRs
   const int N = net.N, H = net.H, T = net.T, M = NF * 32, RP = net.RP, MPW = net.MPW, ND = net.ND;
@@ -1129,7 +1132,7 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
     const bool need_h = k + 1 < net.K;
     // stage this block's chain biases and the w_d / w_g / w_x vectors in LDS (read by every edge tile)
     {
-      const float* be = (kSplitG || Geo<NF, NT>::kSplitT) ? bw.be_u : bw.be;
+      const float* be = (kSplitG || Geo<NF, NT, P>::kSplitT) ? bw.be_u : bw.be;
       const float* wd = kSplitG ? bw.wd_u : bw.wd;
       const float* wg = kSplitG ? bw.wg_u : bw.wg;
       const float* wx = kSplitG ? bw.wx_u : bw.wx;
@@ -1163,7 +1166,7 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
 #endif
     {
       const int elane = opaque_tid() & 63;
-      for (int tile = wave; tile < ntiles_run; tile += kNW) edge_tile<NF, NT, L, D>(net, bw, s, tile, elane, need_h);
+      for (int tile = wave; tile < ntiles_run; tile += kNW) edge_tile<NF, NT, L, D, P>(net, bw, s, tile, elane, need_h);
     }
     __syncthreads();
     STAMP(s, kStEdge);

@@ -12,7 +12,8 @@ from typing import Optional
 LIB_NAME = "libecnf_hip.so"
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 
-ECNF_OK, ECNF_E_INVALID, ECNF_E_UNSUPPORTED, ECNF_E_HIP, ECNF_E_MAX_STEPS = 0, 1, 2, 3, 4
+ECNF_OK, ECNF_E_INVALID, ECNF_E_UNSUPPORTED, ECNF_E_HIP, ECNF_E_MAX_STEPS, ECNF_E_NONFINITE = 0, 1, 2, 3, 4, 5
+PREC_SPLIT_F16, PREC_FP32 = 0, 1
 SOLVER_EULER, SOLVER_DOPRI5 = 0, 1
 DIV_NONE, DIV_HUTCHINSON, DIV_EXACT = 0, 1, 2
 CHAIN_FP32_MFMA, CHAIN_SPLIT_BF16, CHAIN_SPLIT_F16 = 0, 1, 2
@@ -22,6 +23,7 @@ EXPORTED_SYMBOLS = (
     "ecnf_abi_version", "ecnf_last_error", "ecnf_param_count", "ecnf_create", "ecnf_destroy",
     "ecnf_vector_field", "ecnf_vf_jvp", "ecnf_integrate", "ecnf_base_sample", "ecnf_base_log_prob",
     "ecnf_molecules_per_workgroup", "ecnf_chain_arithmetic", "ecnf_target_log_prob", "ecnf_lse_partials",
+    "ecnf_set_precision", "ecnf_get_precision",
 )
 
 TARGET_LJ, TARGET_DW = 0, 1
@@ -69,6 +71,7 @@ class EcnfTarget(ctypes.Structure):
         ("b", ctypes.c_float),
         ("c", ctypes.c_float),
         ("d0", ctypes.c_float),
+        ("r_nodes", ctypes.c_void_p),
     ]
 
 
@@ -111,6 +114,8 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
         "ecnf_chain_arithmetic": ([P, I32, ctypes.POINTER(I32)], ctypes.c_int),
         "ecnf_target_log_prob": ([ctypes.POINTER(EcnfTarget), P, P, I32, P], ctypes.c_int),
         "ecnf_lse_partials": ([P, P, I32, P, P], ctypes.c_int),
+        "ecnf_set_precision": ([P, I32], ctypes.c_int),
+        "ecnf_get_precision": ([P, ctypes.POINTER(I32)], ctypes.c_int),
     }
     for name, (argtypes, restype) in sig.items():
         fn = getattr(lib, name)

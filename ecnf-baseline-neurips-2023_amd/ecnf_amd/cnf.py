@@ -17,6 +17,7 @@ Differences, all deliberate and documented in DESIGN.md:
 """
 from __future__ import annotations
 
+import hashlib
 from functools import partial
 from typing import Callable, Mapping, NamedTuple, Optional, Sequence, Tuple, Union
 
@@ -25,13 +26,13 @@ import torch
 
 from . import _lib
 from .engine import EcnfHandle, SolveOptions
-from .params import CNFConfig, init_params
+from .params import CNFConfig, flatten_params, init_params
 
 Params = Union[Mapping, np.ndarray, EcnfHandle]
 
 
 class FlowMatchingCNF(NamedTuple):
-    """core.py:42-49 (+ ``cfg`` and ``device``)."""
+    """core.py:42-49 (+ ``cfg``, ``device`` and ``to_device``: params -> an explicit EcnfHandle)."""
     init: Callable
     apply: Callable
     sample_base: Callable
@@ -40,6 +41,7 @@ class FlowMatchingCNF(NamedTuple):
     sample_and_log_prob_base: Callable
     cfg: CNFConfig
     device: torch.device
+    to_device: Callable
 
 
 def optimal_transport_conditional_vf(x0, x1, t, sigma_min: float):
@@ -53,24 +55,34 @@ def optimal_transport_conditional_vf(x0, x1, t, sigma_min: float):
 
 
 # --------------------------------------------------------------------------------------------------
-# params -> device handle (uploaded once, cached by identity)
+# params -> device handle (uploaded once per distinct CONTENT)
 # --------------------------------------------------------------------------------------------------
-_HANDLE_CACHE: "dict[tuple, tuple]" = {}
+_HANDLE_CACHE: "dict[tuple, EcnfHandle]" = {}
 _CACHE_MAX = 8
 
 
+def params_digest(params: Union[Mapping, np.ndarray], cfg: CNFConfig) -> str:
+    """Content hash of the flat (ravel_pytree-ordered) params blob: a dict updated in place, or a new dict with
+    the same values, maps to the handle holding exactly these weights."""
+    blob = params if isinstance(params, np.ndarray) else flatten_params(params, cfg)
+    blob = np.ascontiguousarray(blob, dtype=np.float32)
+    return hashlib.blake2b(blob.view(np.uint8), digest_size=16).hexdigest()
+
+
 def device_params(params: Params, cfg: CNFConfig, device: torch.device) -> EcnfHandle:
-    """Upload ``params`` (flax-path dict, nested flax dict or flat blob) once; reuse the handle afterwards."""
+    """Upload ``params`` (flax-path dict, nested flax dict or flat blob) to a handle, reusing the handle of an
+    earlier upload with identical content (blake2b of the flat blob; the hash costs ~1 ms per MB of weights per
+    call -- pass an :class:`EcnfHandle` (``to_device``) to skip it).  An EcnfHandle is used as is."""
     if isinstance(params, EcnfHandle):
         return params
-    key = (id(params), cfg, str(device))
+    key = (params_digest(params, cfg), cfg, str(device))
     hit = _HANDLE_CACHE.get(key)
-    if hit is not None and hit[0] is params:
-        return hit[1]
+    if hit is not None:
+        return hit
     h = EcnfHandle(cfg, params, device)
     if len(_HANDLE_CACHE) >= _CACHE_MAX:
-        _HANDLE_CACHE.pop(next(iter(_HANDLE_CACHE)))
-    _HANDLE_CACHE[key] = (params, h)
+        _HANDLE_CACHE.pop(next(iter(_HANDLE_CACHE)))   # freed by its __del__ once no caller holds it
+    _HANDLE_CACHE[key] = h
     return h
 
 
@@ -154,7 +166,7 @@ def build_cnf(n_frames: int, dim: int, sigma_min: float, base_scale: float, n_bl
     return FlowMatchingCNF(init=init, apply=apply, sample_base=sample_base,
                            get_x_t_and_conditional_u_t=partial(optimal_transport_conditional_vf, sigma_min=sigma_min),
                            log_prob_base=log_prob_base, sample_and_log_prob_base=sample_and_log_prob_base,
-                           cfg=cfg, device=dev)
+                           cfg=cfg, device=dev, to_device=lambda params: device_params(params, cfg, dev))
 
 
 def _param_count(cfg):

@@ -42,7 +42,13 @@ def global_normal(n_total: int, event_dim: int, seed: int, lo: int, hi: int, dev
 
 def _allreduce(t: torch.Tensor, op) -> torch.Tensor:
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-        dist.all_reduce(t, op=op)
+        if t.is_cuda and dist.get_backend() == "gloo":
+            # gloo rehearsals (tests, several ranks folded onto one GPU): reduce a host copy
+            h = t.cpu()
+            dist.all_reduce(h, op=op)
+            t.copy_(h)
+        else:
+            dist.all_reduce(t, op=op)
     return t
 
 
@@ -73,10 +79,15 @@ def combine_partials(p: torch.Tensor) -> torch.Tensor:
     p = p.detach().to(torch.float64).reshape(7)
     m_local = p[[0, 2, 4]]
     m = _allreduce(m_local.clone(), dist.ReduceOp.MAX)
-    m0 = torch.where(torch.isfinite(m), m, torch.zeros_like(m))
-    scale = torch.where(torch.isfinite(m_local), torch.exp(m_local - m0), torch.zeros_like(m_local))
+    finite = torch.isfinite(m)
+    m0 = torch.where(finite, m, torch.zeros_like(m))
+    # a rank whose maximum is the global one contributes its sum as is (this also keeps +inf maxima, whose sums
+    # count the +inf entries, free of exp(inf - inf)); empty ranks (-inf) contribute nothing
+    scale = torch.where(m_local == m, torch.ones_like(m_local),
+                        torch.where(torch.isfinite(m_local), torch.exp(m_local - m0), torch.zeros_like(m_local)))
     s = _allreduce(torch.cat([p[[1, 3, 5]] * scale, p[6:7]]), dist.ReduceOp.SUM)
-    return torch.cat([m0 + torch.log(s[:3]), s[3:]])
+    # jax.nn.logsumexp: a +inf maximum gives +inf, no entries (-inf) gives -inf, NaN stays NaN
+    return torch.cat([torch.where(finite, m0 + torch.log(s[:3]), m), s[3:]])
 
 
 def ess_from_device(log_w: torch.Tensor, mask: Optional[torch.Tensor] = None):

@@ -47,10 +47,17 @@ class SolveOptions:
         return o
 
 
-class EcnfHandle:
-    """Owns the device copy of the params (repacked into MFMA fragment order by ecnf_create)."""
+PRECISIONS = {"split_f16": _lib.PREC_SPLIT_F16, "fp32": _lib.PREC_FP32}
 
-    def __init__(self, cfg: CNFConfig, params: Union[Mapping, np.ndarray], device: Union[int, torch.device] = 0):
+
+class EcnfHandle:
+    """Owns the device copy of the params (repacked into MFMA fragment order by ecnf_create).
+
+    precision: "split_f16" (default; fp32 operands split into fp16 pieces on the 16-bit matrix cores) or "fp32"
+    (every GEMM on the fp32 matrix cores) -- include/ecnf.h ecnf_precision."""
+
+    def __init__(self, cfg: CNFConfig, params: Union[Mapping, np.ndarray], device: Union[int, torch.device] = 0,
+                 precision: str = "split_f16"):
         if not torch.cuda.is_available():
             raise RuntimeError("ecnf_amd needs a ROCm GPU (torch.cuda.is_available() is False)")
         self.lib = _lib.load()
@@ -70,6 +77,13 @@ class EcnfHandle:
         _lib.check(self.lib.ecnf_create(ctypes.byref(self._c), blob.ctypes.data, blob.size, self.device.index,
                                         ctypes.byref(h)))
         self._h = h
+        self.set_precision(precision)
+
+    def set_precision(self, precision: str) -> None:
+        if precision not in PRECISIONS:
+            raise ValueError(f"precision must be one of {sorted(PRECISIONS)}")
+        _lib.check(self.lib.ecnf_set_precision(self._h, PRECISIONS[precision]))
+        self.precision = precision
 
     def close(self):
         if getattr(self, "_h", None) is not None and self._h.value:
@@ -97,20 +111,21 @@ class EcnfHandle:
         if feat is None:
             # build_cnf.py:74 asserts rank 2 on node_features: the EGNN field has no features=None path
             raise ValueError("features must be given for the EGNN vector field (build_cnf.py:73-75)")
-        f = torch.as_tensor(feat, device=self.device)
+        on_device = torch.is_tensor(feat) and feat.is_cuda
+        f = torch.as_tensor(feat)
+        if f.dtype.is_floating_point:
+            raise ValueError("features are integer embedding ids")
+        if not on_device and f.numel() and (int(f.min()) < 0 or int(f.max()) >= self.cfg.n_features):
+            # host input: validated here, before the upload.  Device inputs are checked by the kernels (status
+            # ECNF_E_INVALID per molecule from integrate, NaN rows from vector_field / jvp): no device-to-host
+            # sync on the call path
+            raise ValueError(f"feature ids must lie in [0, {self.cfg.n_features})")
+        f = f.to(self.device)
         if f.dim() == 1:
             f = f.reshape(1, -1).expand(batch, -1)
         if f.numel() != batch * N:
             raise ValueError(f"features must have {N} entries per molecule")
-        f = f.reshape(batch, N)
-        if f.shape[1] != N:
-            raise ValueError(f"features must have {N} entries per molecule, got {f.shape[1]}")
-        if f.dtype.is_floating_point:
-            raise ValueError("features are integer embedding ids")
-        f = f.to(torch.int32).contiguous()
-        if f.numel() and (int(f.min()) < 0 or int(f.max()) >= self.cfg.n_features):
-            raise ValueError(f"feature ids must lie in [0, {self.cfg.n_features})")
-        return f
+        return f.reshape(batch, N).to(torch.int32).contiguous()
 
     def molecules_per_workgroup(self, with_tangent: bool = False) -> int:
         v = ctypes.c_int32()
@@ -118,8 +133,8 @@ class EcnfHandle:
         return v.value
 
     def chain_arithmetic(self, with_tangent: bool = False) -> str:
-        """'split_f16' (2-piece fp16 split, 3 cross terms), 'split_bf16' (3-piece bf16 split, 6 cross terms; both
-        chain_split.hpp) or 'fp32_mfma'."""
+        """Edge-chain arithmetic at the current precision: 'split_f16' (2-piece fp16 split, 3 cross terms),
+        'split_bf16' (3-piece bf16 split, 6 cross terms; both chain_split.hpp) or 'fp32_mfma'."""
         v = ctypes.c_int32()
         _lib.check(self.lib.ecnf_chain_arithmetic(self._h, int(with_tangent), ctypes.byref(v)))
         return {_lib.CHAIN_SPLIT_BF16: "split_bf16", _lib.CHAIN_SPLIT_F16: "split_f16"}.get(v.value, "fp32_mfma")
@@ -154,8 +169,14 @@ class EcnfHandle:
         return v, ju
 
     def integrate(self, y0, feat, t0: float, t1: float, opts: SolveOptions, divergence: int = _lib.DIV_NONE,
-                  eps=None, check_status: bool = True):
-        """One-launch ODE solve for the whole batch.  Returns (y1, dlogp or None, nfe, status)."""
+                  eps=None, check_status: bool = True, fallback: bool = True):
+        """One-launch ODE solve for the whole batch.  Returns (y1, dlogp or None, nfe, status).
+
+        check_status: read the per-molecule status back (one sync) and raise like diffrax / chex would:
+        ECNF_E_MAX_STEPS -> RuntimeError, ECNF_E_INVALID (embedding ids out of range) -> ValueError.
+        fallback (with check_status, split_f16 precision): molecules that report ECNF_E_NONFINITE (an activation
+        beyond the fp16 range of the split GEMMs) are solved again on the strict-fp32 kernels and replaced; a
+        molecule that is still non-finite raises."""
         y0 = self._f32(y0, (self.cfg.event_dim,), "y0")
         B = y0.shape[0]
         f = self._feat(feat, B)
@@ -166,6 +187,36 @@ class EcnfHandle:
             e = self._f32(eps, (self.cfg.event_dim,), "eps")
             if e.shape[0] != B:
                 raise ValueError("eps batch mismatch")
+        y1, dl, nfe, status = self._integrate(y0, f, e, t0, t1, opts, divergence)
+        if check_status and B:
+            bad = status != _lib.ECNF_OK
+            if bool(bad.any()):
+                st = status.cpu()
+                if fallback and self.precision == "split_f16" and bool((st == _lib.ECNF_E_NONFINITE).any()):
+                    idx = torch.nonzero(status == _lib.ECNF_E_NONFINITE).reshape(-1)
+                    self.set_precision("fp32")
+                    try:
+                        r = self._integrate(y0[idx].contiguous(), f[idx].contiguous(),
+                                            None if e is None else e[idx].contiguous(), t0, t1, opts, divergence)
+                    finally:
+                        self.set_precision("split_f16")
+                    y1[idx], nfe[idx], status[idx] = r[0], r[2], r[3]
+                    if dl is not None:
+                        dl[idx] = r[1]
+                    st = status.cpu()
+                if bool((st == _lib.ECNF_E_INVALID).any()):
+                    raise ValueError(f"feature ids must lie in [0, {self.cfg.n_features})")
+                n_ms = int((st == _lib.ECNF_E_MAX_STEPS).sum())
+                if n_ms:
+                    # diffrax raises when max_steps is exceeded
+                    raise RuntimeError(f"{n_ms} molecule(s) exceeded max_steps={opts.max_steps}")
+                n_nf = int((st == _lib.ECNF_E_NONFINITE).sum())
+                if n_nf:
+                    raise RuntimeError(f"{n_nf} molecule(s) ended with a non-finite state")
+        return y1, dl, nfe, status
+
+    def _integrate(self, y0, f, e, t0, t1, opts: SolveOptions, divergence: int):
+        B = y0.shape[0]
         y1 = torch.empty_like(y0)
         dl = torch.empty(B, device=self.device, dtype=torch.float32) if divergence != _lib.DIV_NONE else None
         nfe = torch.empty(B, device=self.device, dtype=torch.int32)
@@ -173,11 +224,6 @@ class EcnfHandle:
         o = opts.to_c(t0, t1, divergence)
         _lib.check(self.lib.ecnf_integrate(self._h, ctypes.byref(o), _ptr(y0), _ptr(f), _ptr(e), _ptr(y1), _ptr(dl),
                                            _ptr(nfe), _ptr(status), B, _stream(self.device)))
-        if check_status and B:
-            bad = int((status != 0).sum())
-            if bad:
-                # diffrax raises when max_steps is exceeded
-                raise RuntimeError(f"{bad} molecule(s) exceeded max_steps={opts.max_steps}")
         return y1, dl, nfe, status
 
     def base_sample(self, z) -> torch.Tensor:

@@ -36,9 +36,14 @@ def _flat(x: torch.Tensor, n_nodes: int, dim: int) -> torch.Tensor:
     return x.float().contiguous() if x.dtype != torch.float32 else x.contiguous()
 
 
-def _log_prob(t: _lib.EcnfTarget, x: torch.Tensor) -> torch.Tensor:
+def _log_prob(t: _lib.EcnfTarget, x: torch.Tensor, r_nodes: Optional[torch.Tensor] = None) -> torch.Tensor:
     lib = _lib.load()
     xf = _flat(x, t.n_nodes, t.dim)
+    if r_nodes is not None:
+        r_nodes = torch.as_tensor(r_nodes, device=xf.device, dtype=torch.float32).reshape(-1).contiguous()
+        if r_nodes.numel() != t.n_nodes:
+            raise ValueError(f"r must be a scalar or have n_nodes = {t.n_nodes} entries")
+        t.r_nodes = r_nodes.data_ptr()
     out = torch.empty(xf.shape[0], device=xf.device, dtype=torch.float32)
     stream = torch.cuda.current_stream(xf.device).cuda_stream
     _lib.check(lib.ecnf_target_log_prob(ctypes.byref(t), xf.data_ptr(), out.data_ptr(), xf.shape[0], stream))
@@ -46,10 +51,13 @@ def _log_prob(t: _lib.EcnfTarget, x: torch.Tensor) -> torch.Tensor:
 
 
 def lj_log_prob(x: torch.Tensor, n_nodes: int = 13, dim: int = 3, epsilon: float = 1.0, tau: float = 1.0,
-                r: float = 1.0, harmonic_potential_coef: float = 0.5) -> torch.Tensor:
-    """leonard_jones.log_prob_fn: -energy(x) for x [..., n_nodes*dim] or [..., n_nodes, dim] (scalar r only)."""
-    return _log_prob(_target(_lib.TARGET_LJ, n_nodes, dim, epsilon=epsilon, tau=tau, r=r,
-                             harmonic_potential_coef=harmonic_potential_coef), x)
+                r=1.0, harmonic_potential_coef: float = 0.5) -> torch.Tensor:
+    """leonard_jones.log_prob_fn: -energy(x) for x [..., n_nodes*dim] or [..., n_nodes, dim]; r is a float or a
+    per-node array [n_nodes] (leonard_jones.py:10-20: pair (receiver i, sender j) uses r[i])."""
+    scalar = isinstance(r, (int, float))
+    t = _target(_lib.TARGET_LJ, n_nodes, dim, epsilon=epsilon, tau=tau, r=float(r) if scalar else 1.0,
+                harmonic_potential_coef=harmonic_potential_coef)
+    return _log_prob(t, x, None if scalar else r)
 
 
 def dw_log_prob(x: torch.Tensor, n_nodes: int = 4, dim: int = 2, temperature: float = 1.0, a: float = 0.0,

@@ -20,7 +20,7 @@
  *   ecnf_target_log_prob         <- target log_prob_fn (-energy) of LJ13 / DW4   
  *                                   ecnf/targets/target_energy/leonard_jones.py:10-35, double_well.py:9-28
  *   ecnf_lse_partials            <- the log-sum-exp reductions behind forward / reverse ESS  (section 8f, rank 2)
- *                                   ecnf/train/evaluation.py:10-22, setup_training.py:182
+ *                                   ecnf/utils/evaluation.py:10-22, setup_training.py:182
  *   ecnf_last_error              <- the chex / diffrax exceptions (trace-time asserts, max_steps)
  *
  * Conventions
@@ -41,15 +41,25 @@
 extern "C" {
 #endif
 
-#define ECNF_ABI_VERSION 1
+#define ECNF_ABI_VERSION 2
 
 enum ecnf_status {
   ECNF_OK = 0,
   ECNF_E_INVALID = 1,      /* bad argument / shape (the reference's chex.assert_* failures) */
   ECNF_E_UNSUPPORTED = 2,  /* a configuration this build has no kernel for */
   ECNF_E_HIP = 3,          /* a HIP runtime error (message in ecnf_last_error) */
-  ECNF_E_MAX_STEPS = 4     /* reported per molecule through ecnf_integrate's `status` output */
+  ECNF_E_MAX_STEPS = 4,    /* reported per molecule through ecnf_integrate's `status` output */
+  ECNF_E_NONFINITE = 5     /* per molecule: the final state (positions or log-density) is not finite, e.g. an
+                              activation beyond the fp16 range (|a| >= 65504) of the split GEMMs; rerun those
+                              molecules with ECNF_PREC_FP32 (ecnf_amd does this automatically) */
 };
+
+/* GEMM arithmetic of a handle's kernels (ecnf_set_precision):
+ *   ECNF_PREC_SPLIT_F16  (default) fp32 operands split into two fp16 pieces, three cross terms on the 16-bit
+ *                        matrix cores with fp32 accumulation (fp32-class accuracy; activations must stay below
+ *                        65504 in magnitude, else the molecule reports ECNF_E_NONFINITE)
+ *   ECNF_PREC_FP32       every GEMM on the fp32 matrix cores (v_mfma_f32_32x32x2_f32): the strict-fp32 path */
+enum ecnf_precision { ECNF_PREC_SPLIT_F16 = 0, ECNF_PREC_FP32 = 1 };
 
 enum ecnf_solver { ECNF_SOLVER_EULER = 0, ECNF_SOLVER_DOPRI5 = 1 };
 enum ecnf_divergence { ECNF_DIV_NONE = 0, ECNF_DIV_HUTCHINSON = 1, ECNF_DIV_EXACT = 2 };
@@ -109,7 +119,7 @@ int ecnf_vf_jvp(ecnf_handle* h, const float* x, const float* t, const int32_t* f
  *   y1   [batch, N*D]  positions at t1
  *   dlogp[batch]       l(t1) with dl/dt = div v, l(t0) = 0 (NULL allowed when divergence == NONE)
  *   nfe  [batch]       vector-field evaluations spent on the molecule (NULL allowed)
- *   status [batch]     ECNF_OK or ECNF_E_MAX_STEPS per molecule (NULL allowed) */
+ *   status [batch]     ECNF_OK, ECNF_E_MAX_STEPS or ECNF_E_NONFINITE per molecule (NULL allowed) */
 int ecnf_integrate(ecnf_handle* h, const ecnf_solve_opts* opts, const float* y0, const int32_t* feat,
                    const float* eps, float* y1, float* dlogp, int32_t* nfe, int32_t* status, int32_t batch,
                    void* stream);
@@ -120,10 +130,15 @@ int ecnf_base_sample(ecnf_handle* h, const float* z, float* x0, int32_t batch, v
 /* log_prob_base(y) [batch] of the scaled zero-CoM Gaussian. */
 int ecnf_base_log_prob(ecnf_handle* h, const float* y, float* log_p, int32_t batch, void* stream);
 
+/* Select the GEMM arithmetic (ecnf_precision) of every later call on this handle; ecnf_get_precision reads it. */
+int ecnf_set_precision(ecnf_handle* h, int32_t precision);
+int ecnf_get_precision(ecnf_handle* h, int32_t* precision);
+
 /* Molecules processed by one workgroup for this handle (diagnostic; kernels pick it from the LDS budget). */
 int ecnf_molecules_per_workgroup(ecnf_handle* h, int32_t with_tangent, int32_t* mpw);
 
-/* Arithmetic of the edge-MLP chain GEMMs (the bulk of the FLOPs) in this handle's kernels (diagnostic):
+/* Arithmetic of the edge-MLP chain GEMMs (the bulk of the FLOPs) in this handle's kernels at its current precision
+ * (diagnostic):
  *   ECNF_CHAIN_FP32_MFMA   v_mfma_f32_32x32x2_f32, fp32 operands
  *   ECNF_CHAIN_SPLIT_BF16  fp32 operands split into three bf16 pieces (RNE), the six cross terms above 2^-25 of
  *                          the product on v_mfma_f32_32x32x16_bf16, fp32 accumulation (fp32-accurate)
@@ -138,8 +153,9 @@ int ecnf_chain_arithmetic(ecnf_handle* h, int32_t with_tangent, int32_t* mode);
 /* ---- targets and eval reductions (no handle needed) ---- */
 enum ecnf_target_kind { ECNF_TARGET_LJ = 0, ECNF_TARGET_DW = 1 };
 
-/* Target energy parameters.  LJ (leonard_jones.py:10-27): epsilon, tau, r (scalar; the reference's per-node r
- * array is not supported), harmonic_coef.  DW (double_well.py:9-19): a, b, c, d0, tau.  Defaults are the
+/* Target energy parameters.  LJ (leonard_jones.py:10-27): epsilon, tau, r (a scalar, or the reference's per-node
+ * array `r: chex.Array` as r_nodes, a DEVICE float[n_nodes]; pair (receiver i, sender j) uses r_i,
+ * leonard_jones.py:14-16,20), harmonic_coef.  DW (double_well.py:9-19): a, b, c, d0, tau.  Defaults are the
  * reference's keyword defaults (LJ: 1, 1, 1, 0.5; DW: 0, -4, 0.9, 4, 1). */
 typedef struct ecnf_target {
   int32_t kind;      /* ecnf_target_kind */
@@ -147,6 +163,7 @@ typedef struct ecnf_target {
   int32_t dim;
   float epsilon, tau, r, harmonic_coef;  /* LJ */
   float a, b, c, d0;                     /* DW (tau shared) */
+  const float* r_nodes;                  /* LJ: per-node r (device, n_nodes floats) or NULL for the scalar r */
 } ecnf_target;
 
 /* log_p[i] = -energy(x[i]) for x [batch, n_nodes*dim] (log_prob_fn of the target).  Pair distances use

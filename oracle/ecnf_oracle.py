@@ -631,7 +631,9 @@ def lj_energy(x, n_nodes, dim, epsilon=1.0, tau=1.0, r=1.0, harmonic_potential_c
     vec = x[:, s] - x[:, rcv]
     x2 = np.sum(vec ** 2, -1)
     d = np.sqrt(np.where(x2 == 0, 1.0, x2))
-    term = (r / d) ** 12 - 2 * (r / d) ** 6
+    r = np.asarray(r, np.float64)
+    rr = r[rcv] if r.ndim else r     # per-node r: the receiver's (leonard_jones.py:14-16,20)
+    term = (rr / d) ** 12 - 2 * (rr / d) ** 6
     e = epsilon / (2 * tau) * term.sum(-1)
     com = x.mean(axis=1, keepdims=True)
     return e + harmonic_potential_coef * np.sum((x - com) ** 2, axis=(-1, -2))
@@ -648,10 +650,14 @@ def dw_energy(x, n_nodes, dim, a=0.0, b=-4.0, c=0.9, d0=4.0, tau=1.0):
 
 
 def _logsumexp(a, b=None):
+    """jax.nn.logsumexp(a, b): the max shift is replaced by 0 when it is not finite, so +inf entries give +inf and
+    -inf entries weight 0 (no exp(inf - inf) = NaN)."""
     a = np.asarray(a, np.float64)
     m = np.max(a)
+    m0 = m if np.isfinite(m) else 0.0
     w = np.ones_like(a) if b is None else np.asarray(b, np.float64)
-    return m + np.log(np.sum(w * np.exp(a - m)))
+    with np.errstate(over="ignore", divide="ignore"):
+        return m0 + np.log(np.sum(w * np.exp(a - m0)))
 
 
 def forward_ess(log_w, mask=None):

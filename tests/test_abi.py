@@ -38,7 +38,7 @@ def test_exports_every_declared_symbol(lib):
     nm = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True).stdout
     exported = set(re.findall(r"\bT (ecnf_\w+)", nm))
     assert declared <= exported, declared - exported
-    assert lib.ecnf_abi_version() == 1
+    assert lib.ecnf_abi_version() == 2
 
 
 @pytest.mark.parametrize("name", list(CONFIGS))

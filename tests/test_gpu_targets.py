@@ -68,3 +68,34 @@ def test_lse_partials_contract_and_errors():
     assert np.isneginf(empty[0]) and empty[1] == 0.0 and empty[6] == 0.0
     with pytest.raises(ValueError):
         T.lj_log_prob(torch.zeros(3, 39), 13, 3)      # host tensor
+
+
+def test_lj13_per_node_r():
+    """leonard_jones.py:10-20 with the array form of r: pair (receiver i, sender j) uses r[i]."""
+    rng = np.random.default_rng(5)
+    x = _cfgs(rng, 257, 13, 3, 1.2)
+    r = (1.0 + 0.1 * rng.standard_normal(13)).astype(np.float32)
+    got = T.lj_log_prob(torch.from_numpy(x).cuda().reshape(257, -1), 13, 3, r=torch.from_numpy(r).cuda()).cpu().numpy()
+    ref = -O.lj_energy(x, 13, 3, r=r)
+    err = np.abs(got - ref) / np.maximum(1.0, np.abs(ref))
+    assert err.max() <= 1e-5, err.max()
+    with pytest.raises(ValueError):
+        T.lj_log_prob(torch.from_numpy(x).cuda(), 13, 3, r=torch.ones(12, device="cuda"))
+
+
+@pytest.mark.parametrize("n", [5, 3000])
+def test_ess_with_infinite_log_weights(n):
+    """-inf log_w (a target energy that overflowed to +inf) has zero weight in the log-sum-exps, as
+    jax.nn.logsumexp gives it: no NaN in either ESS (lse_push started from -inf)."""
+    rng = np.random.default_rng(n)
+    lw = (rng.standard_normal(n) * 2.0).astype(np.float32)
+    lw[[0, n // 2, n - 1]] = -np.inf
+    fwd, rev = D.ess_from_device(torch.from_numpy(lw).cuda())
+    rev_ref, fwd_ref = O.reverse_ess(lw), O.forward_ess(lw)
+    assert np.isfinite(float(rev)) and abs(float(rev) - rev_ref) <= 1e-5 * rev_ref
+    assert float(fwd) == fwd_ref == 0.0                     # LSE(-log_w) = +inf
+    p = T.lse_partials(torch.from_numpy(lw).cuda()).cpu().numpy()
+    assert np.isfinite(p[:2]).all() and np.isposinf(p[2]) and p[3] == 3.0 and p[6] == n
+    # an all -inf input: an empty log-sum-exp, not NaN
+    q = T.lse_partials(torch.full((7,), -np.inf, device="cuda")).cpu().numpy()
+    assert np.isneginf(q[0]) and q[1] == 0.0 and np.isposinf(q[2]) and q[3] == 7.0
