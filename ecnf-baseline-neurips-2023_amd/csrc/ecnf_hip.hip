@@ -189,6 +189,18 @@ int fail(int code, const std::string& msg) {
   return code;
 }
 
+}  // namespace
+
+// shared with the training translation unit (ecnf_train.hip): sets the thread-local ecnf_last_error() text
+namespace ecnf {
+int set_error(int code, const char* msg) {
+  g_err = msg;
+  return code;
+}
+}  // namespace ecnf
+
+namespace {
+
 #define HIP_TRY(expr)                                                                         \
   do {                                                                                        \
     hipError_t e_ = (expr);                                                                   \
@@ -692,6 +704,31 @@ int ecnf_create(const ecnf_cfg* cfg, const float* params, size_t n_floats, int d
   *out = h;
   g_err.clear();
   return ECNF_OK;
+}
+
+int ecnf_update_params(ecnf_handle* h, const float* params, int32_t on_device) {
+  if (!h || !params) return fail(ECNF_E_INVALID, "NULL argument");
+  const size_t n = param_count(h->cfg);
+  std::vector<float> host;
+  const float* src = params;
+  HIP_TRY(hipSetDevice(h->device));
+  if (on_device) {
+    host.resize(n);
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(host.data(), params, n * sizeof(float), hipMemcpyDeviceToHost));
+    src = host.data();
+  }
+  // pack into a fresh handle, then take over its weight buffer and kernel arguments
+  ecnf_handle* t = nullptr;
+  const int rc = ecnf_create(&h->cfg, src, n, h->device, &t);
+  if (rc) return rc;
+  HIP_TRY(hipDeviceSynchronize());   // no launch on h's old weights is in flight
+  std::swap(h->dbuf, t->dbuf);
+  for (int i = 0; i < 4; ++i) {
+    h->net[i] = t->net[i];
+    h->lds[i] = t->lds[i];
+  }
+  return ecnf_destroy(t);
 }
 
 int ecnf_destroy(ecnf_handle* h) {

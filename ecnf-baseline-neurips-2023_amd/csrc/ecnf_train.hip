@@ -1,0 +1,954 @@
+// ecnf_train.hip — the flow-matching training step of the EGNN vector field on MI355X (gfx950).
+//
+// Restates, with reverse-mode derivatives written out by hand (no autodiff framework):
+//   flow_matching_loss_fn      ecnf/cnf/loss.py:10-32        loss = mean((v(x_t, t) - u_t)^2),
+//                              ecnf/cnf/core.py:35-39        x_t = (1 - (1 - sigma) t) x0 + t x1, u_t = x1 - (1 - sigma) x0
+//   jax.grad(loss, params)     ecnf/cnf/gradient_step.py:30-36
+//   optax.adam + apply_updates ecnf/cnf/gradient_step.py:38-40, setup_training.py:100-109 (+ EMA :43-47)
+// through FlatEgnn (build_cnf.py:68-93), EGNN.call_single (egnn.py:144-190), EGCL (egnn.py:49-114) and MLP
+// (mlp.py:7-19).
+//
+// Design.  Training batches are small (lj13.yaml: 64 molecules, 9984 edges), so the step is a stream of layered
+// kernels over HBM-resident activations rather than one fused kernel: every dense layer is a strict-fp32 GEMM on
+// v_mfma_f32_32x32x2_f32 (gemm_kernel: 64x64 tiles, 4 waves of 32x32, LDS-staged 16-deep k tiles) with a fused
+// epilogue (bias, residual, SiLU / SiLU' ), weight gradients are split-K GEMMs reduced in a fixed order, and the
+// graph operations (edge gathers, receiver / sender segment sums, shifts, gate) are one thread per output element
+// summing a fixed edge order.  Every gradient entry is written exactly once: the step is deterministic (bitwise
+// run-to-run) and allocation-free after ecnf_trainer_create.
+//
+// Activations saved per block k for the backward pass (B molecules, BN = B N node rows, BE = B N (N-1) edge rows):
+//   hin [BN][H+T], h1 [BN][H], xc [BN][D] (per block input), P_s / P_r [BN][M], r [BE][D], len [BE],
+//   z_e / a_e [L][BE][M] (phi_e), z_x / a_x [L][BE][M] (phi_x torso), px [BE], g [BE], hcat [BN][M+H],
+//   z_h / a_h [L+1][BN][M|H] (phi_h)
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/ecnf.h"
+
+namespace ecnf {
+int set_error(int code, const char* msg);   // ecnf_hip.hip
+}
+
+namespace ecnf_train {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ float sigm(float z) { return 1.0f / (1.0f + __expf(-z)); }
+__device__ __forceinline__ float silu(float z) { return z * sigm(z); }
+__device__ __forceinline__ float dsilu(float z) {
+  const float s = sigm(z);
+  return s * (1.0f + z * (1.0f - s));
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// GEMM: C[M][N] = alpha op(A)[M][K] op(B)[K][N] (+ bias[N]) (+ R) (+ C if accumulate), then optionally
+// z *= silu'(Zs) (the backward of a SiLU layer) and Aout = silu(z) (the forward one, C keeps the pre-activation).
+// TA: A stored [K][M] (lda over m); TB: B stored [N][K].  ksplit > 1: block z sums its k-range into the partial
+// C + z * split_stride (no epilogue), combined by reduce_splits in split order.
+// ---------------------------------------------------------------------------------------------------------------
+struct GemmArgs {
+  int M, N, K;
+  const float* A; long lda;
+  const float* B; long ldb;
+  float* C; long ldc;
+  float alpha;
+  const float* bias;
+  const float* R; long ldr;
+  const float* Zs; long ldz;
+  float* Aout; long ldo;
+  int accumulate;
+  int ksplit; long split_stride;
+};
+
+constexpr int GT = 64, GK = 16;
+
+template <bool TA, bool TB>
+__global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
+  __shared__ float As[GK][GT + 1];
+  __shared__ float Bs[GK][GT + 1];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int m0 = blockIdx.y * GT, n0 = blockIdx.x * GT;
+  const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
+  int kb = 0, ke = g.K;
+  if (g.ksplit > 1) {
+    const int kc = (((g.K + g.ksplit - 1) / g.ksplit) + GK - 1) / GK * GK;
+    kb = blockIdx.z * kc;
+    ke = min(g.K, kb + kc);
+  }
+  f32x16 acc = {};
+  for (int k0 = kb; k0 < ke; k0 += GK) {
+    for (int i = tid; i < GT * GK; i += 256) {
+      int mm, kk;
+      if (TA) { mm = i % GT; kk = i / GT; } else { kk = i % GK; mm = i / GK; }
+      const int gm = m0 + mm, gk = k0 + kk;
+      float v = 0.f;
+      if (gm < g.M && gk < ke) v = TA ? g.A[(long)gk * g.lda + gm] : g.A[(long)gm * g.lda + gk];
+      As[kk][mm] = v;
+    }
+    for (int i = tid; i < GT * GK; i += 256) {
+      int nn, kk;
+      if (TB) { kk = i % GK; nn = i / GK; } else { nn = i % GT; kk = i / GT; }
+      const int gn = n0 + nn, gk = k0 + kk;
+      float v = 0.f;
+      if (gn < g.N && gk < ke) v = TB ? g.B[(long)gn * g.ldb + gk] : g.B[(long)gk * g.ldb + gn];
+      Bs[kk][nn] = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < GK; kk += 2) {
+      const float a = As[kk + (lane >> 5)][wm + (lane & 31)];
+      const float b = Bs[kk + (lane >> 5)][wn + (lane & 31)];
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  const int col = n0 + wn + (lane & 31);
+  if (col >= g.N) return;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int row = m0 + wm + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+    if (row >= g.M) continue;
+    float z = g.alpha * acc[r];
+    if (g.ksplit > 1) {
+      g.C[blockIdx.z * g.split_stride + (long)row * g.ldc + col] = z;
+      continue;
+    }
+    if (g.bias) z += g.bias[col];
+    if (g.R) z += g.R[(long)row * g.ldr + col];
+    if (g.accumulate) z += g.C[(long)row * g.ldc + col];
+    if (g.Zs) z *= dsilu(g.Zs[(long)row * g.ldz + col]);
+    g.C[(long)row * g.ldc + col] = z;
+    if (g.Aout) g.Aout[(long)row * g.ldo + col] = silu(z);
+  }
+}
+
+// dst[i] (+)= sum_s P[s][i], s in order
+__global__ void reduce_splits(const float* __restrict__ P, int S, long n, float* dst, int accumulate) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float acc = 0.f;
+  for (int s = 0; s < S; ++s) acc += P[(long)s * n + i];
+  dst[i] = accumulate ? dst[i] + acc : acc;
+}
+
+// column sums of X[rows][cols] (ld) in row chunks of 256: part[chunk][c]
+__global__ void colsum_kernel(const float* __restrict__ X, int rows, int cols, long ld, float* part) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= cols) return;
+  const int r0 = blockIdx.y * 256, r1 = min(rows, r0 + 256);
+  float acc = 0.f;
+  for (int r = r0; r < r1; ++r) acc += X[(long)r * ld + c];
+  part[(long)blockIdx.y * cols + c] = acc;
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// model geometry: molecule b, receiver i, slot j -> edge row b E + i (N-1) + j, sender (i + 1 + j) mod N
+// (graph.py:6-14); node row b N + i
+// ---------------------------------------------------------------------------------------------------------------
+struct Geom {
+  int B, N, D, H, T, M, L, K, E, nfeat;
+  float C, sigma;
+};
+
+__device__ __forceinline__ int sender_of(int i, int j, int N) {
+  int s = i + 1 + j;
+  return s >= N ? s - N : s;
+}
+// edge slot of (receiver i, sender s != i)
+__device__ __forceinline__ int slot_of(int i, int s, int N) {
+  int j = s - i - 1;
+  return j < 0 ? j + N : j;
+}
+
+struct Freqs {
+  float f[8];   // exp(-k ln(1e4) / (T/2 - 1)) in fp32 (build_cnf.py:23-27)
+};
+
+// x_t, u_t (core.py:35-39), input mean, centred positions (egnn.py:160), time embedding (build_cnf.py:18-32)
+__global__ void k_prologue(Geom G, const float* __restrict__ x1, const float* __restrict__ x0,
+                           const float* __restrict__ t, Freqs freqs, float* ut, float* mean, float* xc0,
+                           float* temb) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= G.B) return;
+  const int ND = G.N * G.D;
+  const float tb = t[b];
+  float mu[3] = {0.f, 0.f, 0.f};
+  for (int i = 0; i < G.N; ++i)
+    for (int d = 0; d < G.D; ++d) {
+      const long o = (long)b * ND + i * G.D + d;
+      const float xt = (1.0f - (1.0f - G.sigma) * tb) * x0[o] + tb * x1[o];
+      ut[o] = x1[o] - (1.0f - G.sigma) * x0[o];
+      xc0[o] = xt;
+      mu[d] += xt;
+    }
+  for (int d = 0; d < G.D; ++d) {
+    mu[d] /= (float)G.N;
+    mean[b * G.D + d] = mu[d];
+  }
+  for (int i = 0; i < G.N; ++i)
+    for (int d = 0; d < G.D; ++d) xc0[(long)b * ND + i * G.D + d] -= mu[d];
+  const int half = G.T / 2;
+  const float ts = tb * 1000.0f;
+  for (int k = 0; k < G.T; ++k) {
+    const float arg = ts * freqs.f[k < half ? k : k - half];
+    temb[b * G.T + k] = k < half ? sinf(arg) : cosf(arg);
+  }
+}
+
+// hin = [h | temb] (h: embedding rows for block 0, else the previous block's output)
+__global__ void k_hin(Geom G, const float* __restrict__ h, long ldh, const int32_t* __restrict__ feat,
+                      const float* __restrict__ emb, const float* __restrict__ temb, float* hin) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int W = G.H + G.T;
+  if (idx >= (long)G.B * G.N * W) return;
+  const long row = idx / W;
+  const int c = (int)(idx - row * W);
+  float v;
+  if (c < G.H) v = feat ? emb[(long)feat[row] * G.H + c] : h[row * ldh + c];
+  else v = temb[(row / G.N) * G.T + (c - G.H)];
+  hin[idx] = v;
+}
+
+// r_ij = x_i - x_j, |r| = safe_norm (egnn.py:73-74, numerical.py:7-10)
+__global__ void k_edge_geom(Geom G, const float* __restrict__ xc, float* r, float* len) {
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (long)G.B * G.E) return;
+  const int b = (int)(e / G.E), el = (int)(e - (long)b * G.E), i = el / (G.N - 1), j = el - i * (G.N - 1);
+  const int s = sender_of(i, j, G.N);
+  float x2 = 0.f;
+  for (int d = 0; d < G.D; ++d) {
+    const float v = xc[((long)b * G.N + i) * G.D + d] - xc[((long)b * G.N + s) * G.D + d];
+    r[e * G.D + d] = v;
+    x2 += v * v;
+  }
+  len[e] = sqrtf(x2 == 0.f ? 1.0f : x2);
+}
+
+// phi_e layer 1 from the per-node halves: z = P_s[s] + P_r[r] + |r|^2 w_d + b; a = silu(z)  (egnn.py:76,79)
+__global__ void k_layer1(Geom G, const float* __restrict__ Ps, const float* __restrict__ Pr,
+                         const float* __restrict__ len, const float* __restrict__ wd, const float* __restrict__ bias,
+                         float* Z, float* A) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long)G.B * G.E * G.M) return;
+  const long e = idx / G.M;
+  const int c = (int)(idx - e * G.M);
+  const int b = (int)(e / G.E), el = (int)(e - (long)b * G.E), i = el / (G.N - 1), j = el - i * (G.N - 1);
+  const int s = sender_of(i, j, G.N);
+  const float l = len[e];
+  const float z = Ps[((long)b * G.N + s) * G.M + c] + Pr[((long)b * G.N + i) * G.M + c] + (l * l) * wd[c] + bias[c];
+  Z[idx] = z;
+  A[idx] = silu(z);
+}
+
+// per edge: px = a_x . w_x + b_x (egnn.py:83-85); gate g = sigmoid(m . w_g + b_g) (egnn.py:99-101).  64 threads
+// per edge (4 edges per 256-thread block)
+__global__ void k_edge_dots(Geom G, const float* __restrict__ ax, const float* __restrict__ wx,
+                            const float* __restrict__ bx, const float* __restrict__ m, const float* __restrict__ wg,
+                            const float* __restrict__ bg, float* px, float* gate) {
+  const long e = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (e >= (long)G.B * G.E) return;
+  float sx = 0.f, sg = 0.f;
+  for (int c = lane; c < G.M; c += 64) {
+    sx += ax[e * G.M + c] * wx[c];
+    if (gate) sg += m[e * G.M + c] * wg[c];
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    sx += __shfl_xor(sx, o);
+    sg += __shfl_xor(sg, o);
+  }
+  if (lane == 0) {
+    px[e] = sx + bx[0];
+    if (gate) gate[e] = sigm(sg + bg[0]);
+  }
+}
+
+// receiver segment sums (e3nn scatter_sum): x_out = x_in + sum_j px r / (C + |r|) / (N - 1) (egnn.py:87-95,113);
+// hcat = [sum_j g m / sqrt(N - 1) | h1] (egnn.py:102-105).  One thread per output element, j in order.
+__global__ void k_node_shift(Geom G, const float* __restrict__ xin, const float* __restrict__ px,
+                             const float* __restrict__ r, const float* __restrict__ len, float* xout) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long)G.B * G.N * G.D) return;
+  const long row = idx / G.D;
+  const int d = (int)(idx - row * G.D);
+  const long e0 = row * (G.N - 1);   // b E + i (N - 1) == (b N + i)(N - 1)
+  float acc = 0.f;
+  for (int j = 0; j < G.N - 1; ++j) {
+    const long e = e0 + j;
+    acc += px[e] * r[e * G.D + d] / (G.C + len[e]);
+  }
+  xout[idx] = xin[idx] + acc / (float)(G.N - 1);
+}
+
+__global__ void k_node_agg(Geom G, const float* __restrict__ m, const float* __restrict__ gate,
+                           const float* __restrict__ h1, float* hcat) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int W = G.M + G.H;
+  if (idx >= (long)G.B * G.N * W) return;
+  const long row = idx / W;
+  const int c = (int)(idx - row * W);
+  if (c >= G.M) {
+    hcat[idx] = h1[row * G.H + (c - G.M)];
+    return;
+  }
+  const long e0 = row * (G.N - 1);
+  float acc = 0.f;
+  for (int j = 0; j < G.N - 1; ++j) acc += m[(e0 + j) * G.M + c] * gate[e0 + j];
+  hcat[idx] = acc / sqrtf((float)(G.N - 1));
+}
+
+// v = ((x_K - x_c0) - mean) fs (egnn.py:183-188), per-molecule partial loss sum((v - u)^2) and d fs, and
+// d loss / d x_K = 2 (v - u) fs / (B N D)
+__global__ void k_output(Geom G, const float* __restrict__ xK, const float* __restrict__ xc0,
+                         const float* __restrict__ mean, const float* __restrict__ ut, const float* __restrict__ fs_p,
+                         float* dxK, float* part_loss, float* part_dfs) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= G.B) return;
+  const float fs = fs_p[0];
+  const int ND = G.N * G.D;
+  const float sc = 2.0f / ((float)G.B * (float)ND);
+  float sl = 0.f, sf = 0.f;
+  for (int k = 0; k < ND; ++k) {
+    const long o = (long)b * ND + k;
+    const float pre = (xK[o] - xc0[o]) - mean[b * G.D + (k % G.D)];
+    const float diff = pre * fs - ut[o];
+    sl += diff * diff;
+    sf += sc * diff * pre;
+    dxK[o] = sc * diff * fs;
+  }
+  part_loss[b] = sl;
+  part_dfs[b] = sf;
+}
+
+__global__ void k_finish_loss(int B, float inv_count, const float* __restrict__ part_loss,
+                              const float* __restrict__ part_dfs, float* loss, float* dfs) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  float a = 0.f, f = 0.f;
+  for (int b = 0; b < B; ++b) {
+    a += part_loss[b];
+    f += part_dfs[b];
+  }
+  *loss = a * inv_count;
+  *dfs = f;
+}
+
+// ---- backward ----
+
+// out[r][c] = X[r][c] (+ Y[r][c])
+__global__ void k_copy_add(long rows, int cols, const float* __restrict__ X, long ldx, const float* __restrict__ Y,
+                           long ldy, float* out, long ldo) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= rows * cols) return;
+  const long r = idx / cols;
+  const int c = (int)(idx - r * cols);
+  out[r * ldo + c] = X[r * ldx + c] + (Y ? Y[r * ldy + c] : 0.0f);
+}
+
+__global__ void k_square(long n, const float* __restrict__ x, float* out) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = x[i] * x[i];
+}
+
+// gate / aggregation backward (egnn.py:99-104): dm_i = dhcat[:, :M] of the receiver; per edge
+// dgm = dm_i / sqrt(N-1); de = (m . dgm) g (1 - g); dm = g dgm + de w_g.  64 threads per edge.
+__global__ void k_gate_bwd(Geom G, const float* __restrict__ m, const float* __restrict__ gate,
+                           const float* __restrict__ dhcat, const float* __restrict__ wg, float* dm, float* de_out) {
+  const long e = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (e >= (long)G.B * G.E) return;
+  const long row = e / (G.N - 1);
+  const float is = 1.0f / sqrtf((float)(G.N - 1));
+  const float* dmi = dhcat + row * (G.M + G.H);
+  float dg = 0.f;
+  for (int c = lane; c < G.M; c += 64) dg += m[e * G.M + c] * (dmi[c] * is);
+  for (int o = 32; o > 0; o >>= 1) dg += __shfl_xor(dg, o);
+  const float gv = gate[e];
+  const float de = dg * gv * (1.0f - gv);
+  for (int c = lane; c < G.M; c += 64) dm[e * G.M + c] = gv * (dmi[c] * is) + de * wg[c];
+  if (lane == 0) de_out[e] = de;
+}
+
+// shift backward (egnn.py:87-95): with dD = d x_out[receiver] / (N - 1), den = C + |r|:
+//   dpx = dD . r / den;  dr = px dD / den - px (r . dD) / den^2 * d|r|/dr  (d|r|/dr = r / |r|, 0 for safe_norm's 1)
+__global__ void k_shift_bwd(Geom G, const float* __restrict__ dxout, const float* __restrict__ px,
+                            const float* __restrict__ r, const float* __restrict__ len, float* dpx, float* dr) {
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (long)G.B * G.E) return;
+  const long row = e / (G.N - 1);
+  const float l = len[e], den = G.C + l, p = px[e];
+  float x2 = 0.f, rd = 0.f, dD[3];
+  for (int d = 0; d < G.D; ++d) {
+    dD[d] = dxout[row * G.D + d] / (float)(G.N - 1);
+    const float rv = r[e * G.D + d];
+    x2 += rv * rv;
+    rd += rv * dD[d];
+  }
+  dpx[e] = rd / den;
+  const float dl = x2 == 0.f ? 0.f : -p * rd / (den * den) / l;
+  for (int d = 0; d < G.D; ++d) dr[e * G.D + d] = p * dD[d] / den + dl * r[e * G.D + d];
+}
+
+// dZ = (dpx w_x) * silu'(Z) for the phi_x torso's last layer (the Dense(1) output's input)
+__global__ void k_outer_dsilu(long rows, int M, const float* __restrict__ dpx, const float* __restrict__ w,
+                              const float* __restrict__ Z, float* dZ) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= rows * M) return;
+  const long e = idx / M;
+  const int c = (int)(idx - e * M);
+  dZ[idx] = dpx[e] * w[c] * dsilu(Z[idx]);
+}
+
+// layer-1 backward, node side: dP_r[i] = sum over the receiver's edges of dz1, dP_s[j] = sum over the sender's
+__global__ void k_layer1_node_bwd(Geom G, const float* __restrict__ dz1, float* dPs, float* dPr) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long)G.B * G.N * G.M) return;
+  const long row = idx / G.M;
+  const int c = (int)(idx - row * G.M);
+  const int b = (int)(row / G.N), n = (int)(row - (long)b * G.N);
+  const long eb = (long)b * G.E;
+  float ar = 0.f, as = 0.f;
+  for (int j = 0; j < G.N - 1; ++j) ar += dz1[(eb + n * (G.N - 1) + j) * G.M + c];
+  for (int i = 0; i < G.N; ++i) {
+    if (i == n) continue;
+    as += dz1[(eb + i * (G.N - 1) + slot_of(i, n, G.N)) * G.M + c];
+  }
+  dPr[idx] = ar;
+  dPs[idx] = as;
+}
+
+// layer-1 backward, edge side: d|r|^2 = dz1 . w_d -> dr += 2 d|r|^2 r (0 for safe_norm's constant branch)
+__global__ void k_layer1_edge_bwd(Geom G, const float* __restrict__ dz1, const float* __restrict__ wd,
+                                  const float* __restrict__ r, float* dr) {
+  const long e = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (e >= (long)G.B * G.E) return;
+  float s = 0.f;
+  for (int c = lane; c < G.M; c += 64) s += dz1[e * G.M + c] * wd[c];
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if (lane == 0) {
+    float x2 = 0.f;
+    for (int d = 0; d < G.D; ++d) x2 += r[e * G.D + d] * r[e * G.D + d];
+    if (x2 != 0.f)
+      for (int d = 0; d < G.D; ++d) dr[e * G.D + d] += 2.0f * s * r[e * G.D + d];
+  }
+}
+
+// positions backward through r_ij = x_i - x_j: dx_in[i] = dx_out[i] + sum_{e: recv i} dr - sum_{e: send i} dr
+__global__ void k_dx_bwd(Geom G, const float* __restrict__ dxout, const float* __restrict__ dr, float* dxin) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long)G.B * G.N * G.D) return;
+  const long row = idx / G.D;
+  const int d = (int)(idx - row * G.D);
+  const int b = (int)(row / G.N), n = (int)(row - (long)b * G.N);
+  const long eb = (long)b * G.E;
+  float a = 0.f;
+  for (int j = 0; j < G.N - 1; ++j) a += dr[(eb + n * (G.N - 1) + j) * G.D + d];
+  float s = 0.f;
+  for (int i = 0; i < G.N; ++i) {
+    if (i == n) continue;
+    s += dr[(eb + i * (G.N - 1) + slot_of(i, n, G.N)) * G.D + d];
+  }
+  dxin[idx] = dxout[idx] + a - s;
+}
+
+// embedding gradient: dEmb[f][c] = sum over node rows with feature f of dhin[row][c] (rows in order)
+__global__ void k_embed_bwd(Geom G, const float* __restrict__ dhin, long ld, const int32_t* __restrict__ feat,
+                            float* demb) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long)G.nfeat * G.H) return;
+  const int f = (int)(idx / G.H), c = (int)(idx - (long)f * G.H);
+  float a = 0.f;
+  const long BN = (long)G.B * G.N;
+  for (long row = 0; row < BN; ++row)
+    if (feat[row] == f) a += dhin[row * ld + c];
+  demb[idx] = a;
+}
+
+// ---- Adam (optax.scale_by_adam + scale(-lr)) and EMA, with the global norms of the gradient and the update ----
+__global__ void k_adam(long n, const float* __restrict__ grad, float* params, float* mu, float* nu, float* ema,
+                       float lr, float b1, float b2, float eps, float eps_root, float bc1, float bc2, float ema_beta,
+                       float* part) {
+  __shared__ float red[2][256];
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  float gg = 0.f, uu = 0.f;
+  if (i < n) {
+    const float gv = grad[i];
+    const float m = b1 * mu[i] + (1.0f - b1) * gv;
+    const float v = b2 * nu[i] + (1.0f - b2) * gv * gv;
+    mu[i] = m;
+    nu[i] = v;
+    const float mh = m / bc1, vh = v / bc2;
+    const float u = -lr * (mh / (sqrtf(vh + eps_root) + eps));
+    const float p = params[i] + u;
+    params[i] = p;
+    if (ema) ema[i] = ema[i] * ema_beta + (1.0f - ema_beta) * p;
+    gg = gv * gv;
+    uu = u * u;
+  }
+  red[0][threadIdx.x] = gg;
+  red[1][threadIdx.x] = uu;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) {
+      red[0][threadIdx.x] += red[0][threadIdx.x + w];
+      red[1][threadIdx.x] += red[1][threadIdx.x + w];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    part[2 * blockIdx.x] = red[0][0];
+    part[2 * blockIdx.x + 1] = red[1][0];
+  }
+}
+
+__global__ void k_norms(int nb, const float* __restrict__ part, float* norms) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  float a = 0.f, b = 0.f;
+  for (int i = 0; i < nb; ++i) {
+    a += part[2 * i];
+    b += part[2 * i + 1];
+  }
+  norms[0] = sqrtf(a);
+  norms[1] = sqrtf(b);
+}
+
+}  // namespace ecnf_train
+
+using namespace ecnf_train;
+
+// ---------------------------------------------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------------------------------------------
+namespace {
+
+// offsets (floats) of every parameter in the flat ravel_pytree blob (flax paths sorted at every level, bias before
+// kernel): EGNN_0/{k}/{Dense_0, Dense_1, phi_e/Dense_l, phi_h/Dense_l, phi_x_torso/Dense_l}, EGNN_0/Dense_k,
+// EGNN_0/final_scaling, Embed_0/embedding (the same walk as ecnf_create)
+struct BlockOff {
+  long xb, xk, gb, gk, eb[4], ek[4], hb[5], hk[5], tb[4], tk[4], nb, nk;
+};
+struct ParamOff {
+  std::vector<BlockOff> blk;
+  long fs, emb, total;
+};
+
+ParamOff param_offsets(const ecnf_cfg& c) {
+  const long H = c.hidden, T = c.time_embedding_dim, M = c.mlp_width, L = c.mlp_depth, K = c.n_blocks;
+  ParamOff o;
+  o.blk.resize(K);
+  long p = 0;
+  auto take = [&](long n) {
+    const long q = p;
+    p += n;
+    return q;
+  };
+  for (int k = 0; k < K; ++k) {
+    BlockOff& b = o.blk[k];
+    b.xb = take(1); b.xk = take(M);
+    b.gb = take(1); b.gk = take(M);
+    for (int l = 0; l < L; ++l) { b.eb[l] = take(M); b.ek[l] = take((l == 0 ? 2 * H + 1 : M) * M); }
+    for (int l = 0; l <= L; ++l) {
+      const long out_f = l == L ? H : M, in_f = l == 0 ? M + H : M;
+      b.hb[l] = take(out_f); b.hk[l] = take(in_f * out_f);
+    }
+    for (int l = 0; l < L; ++l) { b.tb[l] = take(M); b.tk[l] = take(M * M); }
+  }
+  for (int k = 0; k < K; ++k) { o.blk[k].nb = take(H); o.blk[k].nk = take((H + T) * H); }
+  o.fs = take(1);
+  o.emb = take((long)c.n_features * H);
+  o.total = p;
+  return o;
+}
+
+int fail(int code, const std::string& msg) { return ecnf::set_error(code, msg.c_str()); }
+
+#define TR_TRY(expr)                                                                                          \
+  do {                                                                                                        \
+    hipError_t e_ = (expr);                                                                                   \
+    if (e_ != hipSuccess) return fail(ECNF_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));          \
+  } while (0)
+
+}  // namespace
+
+struct ecnf_trainer {
+  ecnf_cfg cfg;
+  int device;
+  int max_batch;
+  ParamOff off;
+  float freqs[8];
+  float* arena;
+  size_t arena_floats;
+  // views into the arena (sized for max_batch)
+  float *ut, *mean, *temb, *part_loss, *part_dfs, *dxa, *dxb, *norm_part;
+  std::vector<float*> xc, hin, h1, Ps, Pr, r, len, px, gate, hcat;   // [K] (xc: [K + 1])
+  std::vector<float*> ze, ae, zx, ax, zh, ah;                        // [K * L], [K * (L + 1)]
+  float *dA, *dB, *dm_gate, *de, *dpx, *dr, *dPs, *dPr, *dhcat, *dh1, *dhin, *dhA, *dhB, *dhn, *split;
+  size_t split_floats;
+};
+
+namespace {
+
+struct Launcher {
+  hipStream_t s;
+  const ecnf_trainer* tr;
+  hipError_t err = hipSuccess;
+
+  void check() {
+    if (err == hipSuccess) err = hipGetLastError();
+  }
+  static unsigned nblk(long n, int t = 256) { return (unsigned)((n + t - 1) / t); }
+
+  // C = op(A) op(B) (+ bias) (+ R) (+ C) (* silu'(Zs)); Aout = silu(C)
+  void gemm(bool ta, bool tb, int M, int N, int K, const float* A, long lda, const float* B, long ldb, float* C,
+            long ldc, const float* bias = nullptr, const float* R = nullptr, long ldr = 0, const float* Zs = nullptr,
+            long ldz = 0, float* Aout = nullptr, long ldo = 0, int accumulate = 0) {
+    GemmArgs g{M, N, K, A, lda, B, ldb, C, ldc, 1.0f, bias, R, ldr, Zs, ldz, Aout, ldo, accumulate, 1, 0};
+    dim3 grid(nblk(N, GT), nblk(M, GT), 1);
+    launch(ta, tb, g, grid);
+  }
+  // weight gradient dW[M][N] (= or +=) A^T dZ over K rows, split over the K dimension, reduced in order
+  void gemm_wgrad(int M, int N, int K, const float* A, long lda, const float* dZ, long ldz, float* dW, long ldw,
+                  int accumulate = 0) {
+    const long n = (long)M * N;
+    int S = (int)std::min<long>(64, std::max<long>(1, K / 256));
+    while (S > 1 && (long)S * n > (long)tr->split_floats) --S;
+    if (S == 1) {
+      GemmArgs g{M, N, K, A, lda, dZ, ldz, dW, ldw, 1.0f, nullptr, nullptr, 0, nullptr, 0, nullptr, 0, accumulate, 1, 0};
+      launch(true, false, g, dim3(nblk(N, GT), nblk(M, GT), 1));
+      return;
+    }
+    GemmArgs g{M, N, K, A, lda, dZ, ldz, tr->split, N, 1.0f, nullptr, nullptr, 0, nullptr, 0, nullptr, 0, 0, S, n};
+    launch(true, false, g, dim3(nblk(N, GT), nblk(M, GT), S));
+    // ldw == N for every weight block of the flat blob (row-major [in][out])
+    hipLaunchKernelGGL(reduce_splits, dim3(nblk(n)), dim3(256), 0, s, tr->split, S, n, dW, accumulate);
+    check();
+  }
+  void colsum(const float* X, int rows, int cols, long ld, float* out) {
+    const int chunks = (rows + 255) / 256;
+    hipLaunchKernelGGL(colsum_kernel, dim3(nblk(cols), chunks), dim3(256), 0, s, X, rows, cols, ld, tr->split);
+    check();
+    hipLaunchKernelGGL(reduce_splits, dim3(nblk(cols)), dim3(256), 0, s, tr->split, chunks, (long)cols, out, 0);
+    check();
+  }
+  void launch(bool ta, bool tb, const GemmArgs& g, dim3 grid) {
+    if (g.M <= 0 || g.N <= 0) return;
+    if (ta && tb) hipLaunchKernelGGL((gemm_kernel<true, true>), grid, dim3(256), 0, s, g);
+    else if (ta) hipLaunchKernelGGL((gemm_kernel<true, false>), grid, dim3(256), 0, s, g);
+    else if (tb) hipLaunchKernelGGL((gemm_kernel<false, true>), grid, dim3(256), 0, s, g);
+    else hipLaunchKernelGGL((gemm_kernel<false, false>), grid, dim3(256), 0, s, g);
+    check();
+  }
+};
+
+}  // namespace
+
+extern "C" {
+
+int ecnf_trainer_create(const ecnf_cfg* cfg, int32_t max_batch, int device, ecnf_trainer** out) {
+  size_t n = 0;
+  int rc = ecnf_param_count(cfg, &n);   // validates the config
+  if (rc) return rc;
+  if (!out) return fail(ECNF_E_INVALID, "out is NULL");
+  if (max_batch < 1) return fail(ECNF_E_INVALID, "max_batch must be >= 1");
+  const ecnf_cfg c = *cfg;
+  const long B = max_batch, N = c.n_nodes, D = c.dim, H = c.hidden, T = c.time_embedding_dim, M = c.mlp_width,
+             L = c.mlp_depth, K = c.n_blocks;
+  const long E = N * (N - 1), BN = B * N, BE = B * E;
+  ecnf_trainer* tr = new ecnf_trainer();
+  tr->cfg = c;
+  tr->device = device;
+  tr->max_batch = max_batch;
+  tr->off = param_offsets(c);
+  const int half = (int)T / 2;
+  const float ex = std::log(10000.0f) / (float)(half - 1);
+  for (int k = 0; k < 8; ++k) tr->freqs[k] = k < half ? std::exp((float)k * -ex) : 0.f;
+  // arena layout
+  std::vector<std::pair<float**, long>> plan;
+  auto add = [&](float** p, long nf) { plan.push_back({p, (nf + 63) & ~63L}); };
+  add(&tr->ut, B * N * D); add(&tr->mean, B * D); add(&tr->temb, B * T);
+  add(&tr->part_loss, B); add(&tr->part_dfs, B); add(&tr->dxa, BN * D); add(&tr->dxb, BN * D);
+  add(&tr->norm_part, 2 * ((n + 255) / 256) + 64);
+  tr->xc.resize(K + 1); tr->hin.resize(K); tr->h1.resize(K); tr->Ps.resize(K); tr->Pr.resize(K); tr->r.resize(K);
+  tr->len.resize(K); tr->px.resize(K); tr->gate.resize(K); tr->hcat.resize(K);
+  tr->ze.resize(K * L); tr->ae.resize(K * L); tr->zx.resize(K * L); tr->ax.resize(K * L);
+  tr->zh.resize(K * (L + 1)); tr->ah.resize(K * (L + 1));
+  for (long k = 0; k <= K; ++k) add(&tr->xc[k], BN * D);
+  for (long k = 0; k < K; ++k) {
+    add(&tr->hin[k], BN * (H + T)); add(&tr->h1[k], BN * H); add(&tr->Ps[k], BN * M); add(&tr->Pr[k], BN * M);
+    add(&tr->r[k], BE * D); add(&tr->len[k], BE); add(&tr->px[k], BE); add(&tr->gate[k], BE);
+    add(&tr->hcat[k], BN * (M + H));
+    for (long l = 0; l < L; ++l) {
+      add(&tr->ze[k * L + l], BE * M); add(&tr->ae[k * L + l], BE * M);
+      add(&tr->zx[k * L + l], BE * M); add(&tr->ax[k * L + l], BE * M);
+    }
+    for (long l = 0; l <= L; ++l) {
+      add(&tr->zh[k * (L + 1) + l], BN * std::max(M, H)); add(&tr->ah[k * (L + 1) + l], BN * M);
+    }
+  }
+  add(&tr->dA, BE * M); add(&tr->dB, BE * M); add(&tr->dm_gate, BE * M); add(&tr->de, BE); add(&tr->dpx, BE);
+  add(&tr->dr, BE * D); add(&tr->dPs, BN * M); add(&tr->dPr, BN * M); add(&tr->dhcat, BN * (M + H));
+  add(&tr->dh1, BN * H); add(&tr->dhin, BN * (H + T)); add(&tr->dhA, BN * M); add(&tr->dhB, BN * M);
+  add(&tr->dhn, BN * H);
+  // split-K / column-sum partials: up to 64 splits of the largest weight block ((M + H) x M or (2H + 1) x M) and
+  // the column-sum chunks of BE rows
+  tr->split_floats = (size_t)std::max<long>(64 * std::max((M + H) * M, (2 * H + 1) * M), ((BE + 255) / 256) * M + M);
+  add(&tr->split, (long)tr->split_floats);
+  size_t total = 0;
+  for (auto& q : plan) total += (size_t)q.second;
+  tr->arena_floats = total;
+  int ndev = 0;
+  hipError_t e = hipGetDeviceCount(&ndev);
+  if (e != hipSuccess || device < 0 || device >= ndev) {
+    delete tr;
+    return e != hipSuccess ? fail(ECNF_E_HIP, std::string("hipGetDeviceCount: ") + hipGetErrorString(e))
+                           : fail(ECNF_E_INVALID, "device index out of range");
+  }
+  if ((e = hipSetDevice(device)) != hipSuccess || (e = hipMalloc(&tr->arena, total * sizeof(float))) != hipSuccess) {
+    delete tr;
+    return fail(ECNF_E_HIP, std::string("trainer allocation: ") + hipGetErrorString(e));
+  }
+  float* p = tr->arena;
+  for (auto& q : plan) {
+    *q.first = p;
+    p += q.second;
+  }
+  *out = tr;
+  return ECNF_OK;
+}
+
+int ecnf_trainer_destroy(ecnf_trainer* tr) {
+  if (!tr) return ECNF_OK;
+  TR_TRY(hipSetDevice(tr->device));
+  TR_TRY(hipDeviceSynchronize());
+  TR_TRY(hipFree(tr->arena));
+  delete tr;
+  return ECNF_OK;
+}
+
+int ecnf_fm_loss_grad(ecnf_trainer* tr, const float* params, const float* x1, const float* x0, const float* t,
+                      const int32_t* feat, float sigma_min, int32_t batch, float* loss, float* grad, void* stream) {
+  if (!tr) return fail(ECNF_E_INVALID, "NULL trainer");
+  if (batch < 1 || batch > tr->max_batch) return fail(ECNF_E_INVALID, "batch must be in [1, max_batch]");
+  if (!params || !x1 || !x0 || !t || !feat || !loss || !grad) return fail(ECNF_E_INVALID, "NULL argument");
+  const ecnf_cfg& c = tr->cfg;
+  Geom G{batch, c.n_nodes, c.dim, c.hidden, c.time_embedding_dim, c.mlp_width, c.mlp_depth, c.n_blocks,
+         c.n_nodes * (c.n_nodes - 1), c.n_features, c.normalization_constant, sigma_min};
+  const long B = batch, N = G.N, D = G.D, H = G.H, T = G.T, M = G.M, L = G.L, K = G.K;
+  const long BN = B * N, BE = B * G.E, ND = N * D;
+  const ParamOff& o = tr->off;
+  const float* P = params;
+  float* dP = grad;
+  TR_TRY(hipSetDevice(tr->device));
+  hipStream_t s = (hipStream_t)stream;
+  Launcher Lc{s, tr};
+  auto nb = [](long n) { return Launcher::nblk(n); };
+  TR_TRY(hipMemsetAsync(grad, 0, (size_t)o.total * sizeof(float), s));
+  Freqs fq;
+  std::memcpy(fq.f, tr->freqs, sizeof(fq.f));
+
+  // ------------------------------------------------------------------ forward
+  hipLaunchKernelGGL(k_prologue, dim3(nb(B)), dim3(256), 0, s, G, x1, x0, t, fq, tr->ut, tr->mean, tr->xc[0],
+                     tr->temb);
+  Lc.check();
+  for (long k = 0; k < K; ++k) {
+    const BlockOff& bo = o.blk[k];
+    // hin = [h | temb]; h1 = hin Wn + bn  (egnn.py:166-167)
+    if (k == 0)
+      hipLaunchKernelGGL(k_hin, dim3(nb(BN * (H + T))), dim3(256), 0, s, G, (const float*)nullptr, 0L, feat,
+                         P + o.emb, (const float*)tr->temb, tr->hin[0]);
+    else
+      hipLaunchKernelGGL(k_hin, dim3(nb(BN * (H + T))), dim3(256), 0, s, G, (const float*)tr->zh[(k - 1) * (L + 1) + L],
+                         H, (const int32_t*)nullptr, (const float*)nullptr, (const float*)tr->temb, tr->hin[k]);
+    Lc.check();
+    Lc.gemm(false, false, (int)BN, (int)H, (int)(H + T), tr->hin[k], H + T, P + bo.nk, H, tr->h1[k], H, P + bo.nb);
+    // per-node halves of phi_e layer 1: P_s = h1 W[0:H], P_r = h1 W[H:2H]
+    Lc.gemm(false, false, (int)BN, (int)M, (int)H, tr->h1[k], H, P + bo.ek[0], M, tr->Ps[k], M);
+    Lc.gemm(false, false, (int)BN, (int)M, (int)H, tr->h1[k], H, P + bo.ek[0] + H * M, M, tr->Pr[k], M);
+    hipLaunchKernelGGL(k_edge_geom, dim3(nb(BE)), dim3(256), 0, s, G, (const float*)tr->xc[k], tr->r[k], tr->len[k]);
+    Lc.check();
+    hipLaunchKernelGGL(k_layer1, dim3(nb(BE * M)), dim3(256), 0, s, G, (const float*)tr->Ps[k],
+                       (const float*)tr->Pr[k], (const float*)tr->len[k], P + bo.ek[0] + 2 * H * M, P + bo.eb[0],
+                       tr->ze[k * L], tr->ae[k * L]);
+    Lc.check();
+    for (long l = 1; l < L; ++l)   // phi_e layers 2..L (egnn.py:79, SiLU after every layer)
+      Lc.gemm(false, false, (int)BE, (int)M, (int)M, tr->ae[k * L + l - 1], M, P + bo.ek[l], M, tr->ze[k * L + l], M,
+              P + bo.eb[l], nullptr, 0, nullptr, 0, tr->ae[k * L + l], M);
+    const float* m = tr->ae[k * L + L - 1];
+    for (long l = 0; l < L; ++l)   // phi_x torso (egnn.py:82)
+      Lc.gemm(false, false, (int)BE, (int)M, (int)M, l == 0 ? m : tr->ax[k * L + l - 1], M, P + bo.tk[l], M,
+              tr->zx[k * L + l], M, P + bo.tb[l], nullptr, 0, nullptr, 0, tr->ax[k * L + l], M);
+    // px and the gate (the gate only feeds h: skipped in the last block, whose h nothing reads)
+    const bool need_h = k + 1 < K;
+    hipLaunchKernelGGL(k_edge_dots, dim3((unsigned)((BE + 3) / 4)), dim3(256), 0, s, G,
+                       (const float*)tr->ax[k * L + L - 1], P + bo.xk, P + bo.xb, m, P + bo.gk, P + bo.gb, tr->px[k],
+                       need_h ? tr->gate[k] : (float*)nullptr);
+    Lc.check();
+    hipLaunchKernelGGL(k_node_shift, dim3(nb(BN * D)), dim3(256), 0, s, G, (const float*)tr->xc[k],
+                       (const float*)tr->px[k], (const float*)tr->r[k], (const float*)tr->len[k], tr->xc[k + 1]);
+    Lc.check();
+    if (need_h) {
+      hipLaunchKernelGGL(k_node_agg, dim3(nb(BN * (M + H))), dim3(256), 0, s, G, m, (const float*)tr->gate[k],
+                         (const float*)tr->h1[k], tr->hcat[k]);
+      Lc.check();
+      // phi_h = MLP((M,) * L + (H,)) on [m_i | h1], residual h1 (egnn.py:105-111)
+      for (long l = 0; l <= L; ++l) {
+        const int in_f = (int)(l == 0 ? M + H : M), out_f = (int)(l == L ? H : M);
+        const float* X = l == 0 ? tr->hcat[k] : tr->ah[k * (L + 1) + l - 1];
+        Lc.gemm(false, false, (int)BN, out_f, in_f, X, in_f, P + bo.hk[l], out_f, tr->zh[k * (L + 1) + l], out_f,
+                P + bo.hb[l], l == L ? tr->h1[k] : nullptr, H, nullptr, 0,
+                l == L ? nullptr : tr->ah[k * (L + 1) + l], out_f);
+      }
+    }
+  }
+  hipLaunchKernelGGL(k_output, dim3(nb(B)), dim3(256), 0, s, G, (const float*)tr->xc[K], (const float*)tr->xc[0],
+                     (const float*)tr->mean, (const float*)tr->ut, P + o.fs, tr->dxa, tr->part_loss, tr->part_dfs);
+  Lc.check();
+  hipLaunchKernelGGL(k_finish_loss, dim3(1), dim3(64), 0, s, (int)B, 1.0f / (float)(B * ND),
+                     (const float*)tr->part_loss, (const float*)tr->part_dfs, loss, dP + o.fs);
+  Lc.check();
+
+  // ------------------------------------------------------------------ backward
+  float* dx = tr->dxa;      // d loss / d x_{k+1}
+  float* dxn = tr->dxb;
+  const float* dh_next = nullptr;   // d loss / d h_new of block k (nullptr: zero, the last block)
+  for (long k = K - 1; k >= 0; --k) {
+    const BlockOff& bo = o.blk[k];
+    const bool need_h = k + 1 < K;
+    const float* m = tr->ae[k * L + L - 1];
+    // dh1 starts from the residual of phi_h (h_new = phi_h(hcat) + h1)
+    if (need_h) {
+      // phi_h backward: dZ_L = dh_new (no final activation)
+      const float* dZ = dh_next;
+      float* bufs[2] = {tr->dhA, tr->dhB};
+      for (long l = L; l >= 0; --l) {
+        const int in_f = (int)(l == 0 ? M + H : M), out_f = (int)(l == L ? H : M);
+        const float* X = l == 0 ? tr->hcat[k] : tr->ah[k * (L + 1) + l - 1];
+        Lc.gemm_wgrad(in_f, out_f, (int)BN, X, in_f, dZ, out_f, dP + bo.hk[l], out_f);
+        Lc.colsum(dZ, (int)BN, out_f, out_f, dP + bo.hb[l]);
+        if (l > 0) {
+          float* dZp = bufs[l & 1];
+          Lc.gemm(false, true, (int)BN, (int)M, out_f, dZ, out_f, P + bo.hk[l], out_f, dZp, M, nullptr, nullptr, 0,
+                  tr->zh[k * (L + 1) + l - 1], M);
+          dZ = dZp;
+        } else {
+          Lc.gemm(false, true, (int)BN, (int)(M + H), (int)M, dZ, M, P + bo.hk[0], M, tr->dhcat, M + H);
+        }
+      }
+      // dh1 = dh_new (the residual) + dhcat[:, M:] (phi_h's input h1)
+      hipLaunchKernelGGL(k_copy_add, dim3(nb(BN * H)), dim3(256), 0, s, BN, (int)H, dh_next, H,
+                         (const float*)(tr->dhcat + M), M + H, tr->dh1, H);
+      Lc.check();
+    }
+    // shifts: dpx, dr (egnn.py:87-95)
+    hipLaunchKernelGGL(k_shift_bwd, dim3(nb(BE)), dim3(256), 0, s, G, (const float*)dx, (const float*)tr->px[k],
+                       (const float*)tr->r[k], (const float*)tr->len[k], tr->dpx, tr->dr);
+    Lc.check();
+    // phi_x output Dense(1): dw_x = a_x[L-1]^T dpx, db_x = sum dpx; dZ_x[L-1] = dpx w_x silu'(z)
+    Lc.gemm_wgrad((int)M, 1, (int)BE, tr->ax[k * L + L - 1], M, tr->dpx, 1, dP + bo.xk, 1);
+    Lc.colsum(tr->dpx, (int)BE, 1, 1, dP + bo.xb);
+    hipLaunchKernelGGL(k_outer_dsilu, dim3(nb(BE * M)), dim3(256), 0, s, BE, (int)M, (const float*)tr->dpx,
+                       P + bo.xk, (const float*)tr->zx[k * L + L - 1], tr->dA);
+    Lc.check();
+    // gate path (egnn.py:99-104) into dm_gate, its weights
+    if (need_h) {
+      hipLaunchKernelGGL(k_gate_bwd, dim3((unsigned)((BE + 3) / 4)), dim3(256), 0, s, G, m,
+                         (const float*)tr->gate[k], (const float*)tr->dhcat, P + bo.gk, tr->dm_gate, tr->de);
+      Lc.check();
+      Lc.gemm_wgrad((int)M, 1, (int)BE, m, M, tr->de, 1, dP + bo.gk, 1);
+      Lc.colsum(tr->de, (int)BE, 1, 1, dP + bo.gb);
+    }
+    // phi_x torso backward: layers L-1 .. 0; the input of layer 0 is m
+    float* dZ = tr->dA;
+    float* other = tr->dB;
+    for (long l = L - 1; l >= 0; --l) {
+      const float* X = l == 0 ? m : tr->ax[k * L + l - 1];
+      Lc.gemm_wgrad((int)M, (int)M, (int)BE, X, M, dZ, M, dP + bo.tk[l], M);
+      Lc.colsum(dZ, (int)BE, (int)M, M, dP + bo.tb[l]);
+      if (l > 0) {
+        Lc.gemm(false, true, (int)BE, (int)M, (int)M, dZ, M, P + bo.tk[l], M, other, M, nullptr, nullptr, 0,
+                tr->zx[k * L + l - 1], M);
+      } else {
+        // d m = dZ_0 W_0^T (+ the gate path), times silu'(z_e[L-1]): the phi_e output layer's dZ
+        Lc.gemm(false, true, (int)BE, (int)M, (int)M, dZ, M, P + bo.tk[0], M, other, M, nullptr,
+                need_h ? tr->dm_gate : nullptr, M, tr->ze[k * L + L - 1], M);
+      }
+      std::swap(dZ, other);
+    }
+    // phi_e backward: layers L-1 .. 1 (layer 0 is the factorised layer 1)
+    for (long l = L - 1; l >= 1; --l) {
+      Lc.gemm_wgrad((int)M, (int)M, (int)BE, tr->ae[k * L + l - 1], M, dZ, M, dP + bo.ek[l], M);
+      Lc.colsum(dZ, (int)BE, (int)M, M, dP + bo.eb[l]);
+      Lc.gemm(false, true, (int)BE, (int)M, (int)M, dZ, M, P + bo.ek[l], M, other, M, nullptr, nullptr, 0,
+              tr->ze[k * L + l - 1], M);
+      std::swap(dZ, other);
+    }
+    // layer 1: dz1 = dZ.  dw_d = |r|^2 . dz1, db, node halves, |r|^2 -> dr
+    {
+      // |r|^2 per edge into `other` (scratch), then dw_d = (|r|^2)^T dz1
+      hipLaunchKernelGGL(k_square, dim3(nb(BE)), dim3(256), 0, s, BE, (const float*)tr->len[k], other);
+      Lc.check();
+      Lc.gemm_wgrad(1, (int)M, (int)BE, other, 1, dZ, M, dP + bo.ek[0] + 2 * H * M, M);
+      Lc.colsum(dZ, (int)BE, (int)M, M, dP + bo.eb[0]);
+      hipLaunchKernelGGL(k_layer1_node_bwd, dim3(nb(BN * M)), dim3(256), 0, s, G, (const float*)dZ, tr->dPs,
+                         tr->dPr);
+      Lc.check();
+      hipLaunchKernelGGL(k_layer1_edge_bwd, dim3((unsigned)((BE + 3) / 4)), dim3(256), 0, s, G, (const float*)dZ,
+                         P + bo.ek[0] + 2 * H * M, (const float*)tr->r[k], tr->dr);
+      Lc.check();
+      Lc.gemm_wgrad((int)H, (int)M, (int)BN, tr->h1[k], H, tr->dPs, M, dP + bo.ek[0], M);
+      Lc.gemm_wgrad((int)H, (int)M, (int)BN, tr->h1[k], H, tr->dPr, M, dP + bo.ek[0] + H * M, M);
+      // dh1 (+)= dP_s W_s^T + dP_r W_r^T
+      Lc.gemm(false, true, (int)BN, (int)H, (int)M, tr->dPs, M, P + bo.ek[0], M, tr->dh1, H, nullptr, nullptr, 0,
+              nullptr, 0, nullptr, 0, need_h ? 1 : 0);
+      Lc.gemm(false, true, (int)BN, (int)H, (int)M, tr->dPr, M, P + bo.ek[0] + H * M, M, tr->dh1, H, nullptr, nullptr,
+              0, nullptr, 0, nullptr, 0, 1);
+    }
+    // positions: dx_k = dx_{k+1} + receiver sums - sender sums of dr
+    hipLaunchKernelGGL(k_dx_bwd, dim3(nb(BN * D)), dim3(256), 0, s, G, (const float*)dx, (const float*)tr->dr, dxn);
+    Lc.check();
+    std::swap(dx, dxn);
+    // node Dense: dWn = hin^T dh1, dbn, dhin = dh1 Wn^T
+    Lc.gemm_wgrad((int)(H + T), (int)H, (int)BN, tr->hin[k], H + T, tr->dh1, H, dP + bo.nk, H);
+    Lc.colsum(tr->dh1, (int)BN, (int)H, H, dP + bo.nb);
+    Lc.gemm(false, true, (int)BN, (int)(H + T), (int)H, tr->dh1, H, P + bo.nk, H, tr->dhin, H + T);
+    dh_next = nullptr;
+    if (k > 0) {
+      // the previous block's h_new gradient: dhin[:, :H] (the temb columns carry no parameters), compacted
+      hipLaunchKernelGGL(k_copy_add, dim3(nb(BN * H)), dim3(256), 0, s, BN, (int)H, (const float*)tr->dhin, H + T,
+                         (const float*)nullptr, 0L, tr->dhn, H);
+      Lc.check();
+      dh_next = tr->dhn;
+    }
+  }
+  hipLaunchKernelGGL(k_embed_bwd, dim3(nb((long)G.nfeat * H)), dim3(256), 0, s, G, (const float*)tr->dhin, H + T,
+                     feat, dP + o.emb);
+  Lc.check();
+  if (Lc.err != hipSuccess) return fail(ECNF_E_HIP, std::string("training step launch: ") + hipGetErrorString(Lc.err));
+  return ECNF_OK;
+}
+
+int ecnf_adam_update(ecnf_trainer* tr, const float* grad, float* params, float* mu, float* nu, float* ema, size_t n,
+                     const ecnf_adam_opts* o, float* norms, void* stream) {
+  if (!tr || !o) return fail(ECNF_E_INVALID, "NULL trainer/options");
+  if ((long)n != tr->off.total) return fail(ECNF_E_INVALID, "n must be the trainer's parameter count");
+  if (!grad || !params || !mu || !nu) return fail(ECNF_E_INVALID, "NULL argument");
+  if (o->count < 1) return fail(ECNF_E_INVALID, "count (the step number after this update) must be >= 1");
+  TR_TRY(hipSetDevice(tr->device));
+  hipStream_t s = (hipStream_t)stream;
+  const unsigned nbk = (unsigned)((n + 255) / 256);
+  const float bc1 = 1.0f - std::pow(o->b1, (float)o->count), bc2 = 1.0f - std::pow(o->b2, (float)o->count);
+  hipLaunchKernelGGL(k_adam, dim3(nbk), dim3(256), 0, s, (long)n, grad, params, mu, nu, ema, o->lr, o->b1, o->b2,
+                     o->eps, o->eps_root, bc1, bc2, o->ema_beta, tr->norm_part);
+  TR_TRY(hipGetLastError());
+  if (norms) {
+    hipLaunchKernelGGL(k_norms, dim3(1), dim3(64), 0, s, (int)nbk, (const float*)tr->norm_part, norms);
+    TR_TRY(hipGetLastError());
+  }
+  return ECNF_OK;
+}
+
+}  // extern "C"

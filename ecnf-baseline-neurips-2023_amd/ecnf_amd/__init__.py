@@ -12,7 +12,7 @@ __all__ = [
 
 def __getattr__(name):
     # torch-dependent modules load lazily so that the layout helpers import without a GPU stack
-    if name in ("cnf", "engine", "distributed", "targets", "dataio"):
+    if name in ("cnf", "engine", "distributed", "targets", "dataio", "train"):
         import importlib
         return importlib.import_module(f".{name}", __name__)
     raise AttributeError(name)

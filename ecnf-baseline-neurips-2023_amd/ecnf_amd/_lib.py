@@ -23,7 +23,8 @@ EXPORTED_SYMBOLS = (
     "ecnf_abi_version", "ecnf_last_error", "ecnf_param_count", "ecnf_create", "ecnf_destroy",
     "ecnf_vector_field", "ecnf_vf_jvp", "ecnf_integrate", "ecnf_base_sample", "ecnf_base_log_prob",
     "ecnf_molecules_per_workgroup", "ecnf_chain_arithmetic", "ecnf_target_log_prob", "ecnf_lse_partials",
-    "ecnf_set_precision", "ecnf_get_precision",
+    "ecnf_set_precision", "ecnf_get_precision", "ecnf_trainer_create", "ecnf_trainer_destroy", "ecnf_fm_loss_grad",
+    "ecnf_adam_update", "ecnf_update_params",
 )
 
 TARGET_LJ, TARGET_DW = 0, 1
@@ -75,6 +76,18 @@ class EcnfTarget(ctypes.Structure):
     ]
 
 
+class EcnfAdamOpts(ctypes.Structure):
+    _fields_ = [
+        ("lr", ctypes.c_float),
+        ("b1", ctypes.c_float),
+        ("b2", ctypes.c_float),
+        ("eps", ctypes.c_float),
+        ("eps_root", ctypes.c_float),
+        ("count", ctypes.c_int32),
+        ("ema_beta", ctypes.c_float),
+    ]
+
+
 class EcnfError(RuntimeError):
     def __init__(self, code: int, msg: str):
         super().__init__(f"ecnf error {code}: {msg}")
@@ -116,6 +129,11 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
         "ecnf_lse_partials": ([P, P, I32, P, P], ctypes.c_int),
         "ecnf_set_precision": ([P, I32], ctypes.c_int),
         "ecnf_get_precision": ([P, ctypes.POINTER(I32)], ctypes.c_int),
+        "ecnf_trainer_create": ([ctypes.POINTER(EcnfCfg), I32, ctypes.c_int, ctypes.POINTER(P)], ctypes.c_int),
+        "ecnf_trainer_destroy": ([P], ctypes.c_int),
+        "ecnf_fm_loss_grad": ([P, P, P, P, P, P, ctypes.c_float, I32, P, P, P], ctypes.c_int),
+        "ecnf_adam_update": ([P, P, P, P, P, P, SZ, ctypes.POINTER(EcnfAdamOpts), P, P], ctypes.c_int),
+        "ecnf_update_params": ([P, P, I32], ctypes.c_int),
     }
     for name, (argtypes, restype) in sig.items():
         fn = getattr(lib, name)

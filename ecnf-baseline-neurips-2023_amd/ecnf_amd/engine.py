@@ -79,6 +79,21 @@ class EcnfHandle:
         self._h = h
         self.set_precision(precision)
 
+    def update_params(self, params) -> None:
+        """Re-pack new weights into this handle (ecnf_update_params): a flax-path dict / flat host blob, or the flat
+        device tensor of a TrainingState."""
+        if torch.is_tensor(params) and params.is_cuda:
+            p = params.to(self.device, torch.float32).contiguous().reshape(-1)
+            if p.numel() != param_count(self.cfg):
+                raise ValueError(f"params blob has {p.numel()} floats, expected {param_count(self.cfg)}")
+            _lib.check(self.lib.ecnf_update_params(self._h, p.data_ptr(), 1))
+            return
+        blob = params if isinstance(params, np.ndarray) else flatten_params(params, self.cfg)
+        blob = np.ascontiguousarray(blob, dtype=np.float32)
+        if blob.size != param_count(self.cfg):
+            raise ValueError(f"params blob has {blob.size} floats, expected {param_count(self.cfg)}")
+        _lib.check(self.lib.ecnf_update_params(self._h, blob.ctypes.data, 0))
+
     def set_precision(self, precision: str) -> None:
         if precision not in PRECISIONS:
             raise ValueError(f"precision must be one of {sorted(PRECISIONS)}")

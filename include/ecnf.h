@@ -175,6 +175,39 @@ int ecnf_target_log_prob(const ecnf_target* t, const float* x, float* log_p, int
  * out is a DEVICE float[7].  Ranks combine partials with one MAX and one SUM all-reduce (ecnf_amd.distributed). */
 int ecnf_lse_partials(const float* v, const float* mask, int32_t n, float* out, void* stream);
 
+/* ---- flow-matching training --------------------------------------------------
+ *   ecnf_fm_loss_grad   <- jax.grad(flow_matching_loss_fn)     ecnf/cnf/loss.py:10-32, cnf/gradient_step.py:30-36
+ *   ecnf_adam_update    <- optax.adam update + apply_updates (+ EMA)   gradient_step.py:38-51, setup_training.py:100-109
+ *   ecnf_update_params  <- the new state.params in cnf.apply (re-packs a sampling handle's weights)
+ * Parameters, gradients and Adam moments are DEVICE flat fp32 blobs in the ravel_pytree order (ecnf_param_count).
+ * Every dense layer runs on the fp32 matrix cores (v_mfma_f32_32x32x2_f32); the step is deterministic. */
+typedef struct ecnf_trainer ecnf_trainer;
+
+/* Workspace for batches of up to max_batch molecules (activations kept for the backward pass). */
+int ecnf_trainer_create(const ecnf_cfg* cfg, int32_t max_batch, int device, ecnf_trainer** out);
+int ecnf_trainer_destroy(ecnf_trainer* tr);
+
+/* loss[0] = mean((v(x_t, t) - u_t)^2) over batch x N*D with x_t = (1 - (1 - sigma_min) t) x0 + t x1,
+ * u_t = x1 - (1 - sigma_min) x0 (core.py:35-39); grad = d loss / d params.  x1 (data), x0 (base sample):
+ * [batch, N*D]; t: [batch]; feat: [batch, N] (ids must lie in [0, n_features)); loss: DEVICE float[1]. */
+int ecnf_fm_loss_grad(ecnf_trainer* tr, const float* params, const float* x1, const float* x0, const float* t,
+                      const int32_t* feat, float sigma_min, int32_t batch, float* loss, float* grad, void* stream);
+
+/* optax.adam(lr, b1, b2, eps, eps_root) at step `count` (1 for the first update: the bias corrections use
+ * 1 - b^count) applied in place: params += -lr mu_hat / (sqrt(nu_hat + eps_root) + eps); ema (optional, may be
+ * NULL) = ema * ema_beta + (1 - ema_beta) * params.  norms (optional): DEVICE float[2] = (|grad|, |update|), the
+ * optax.global_norm values of gradient_step.py:41-44. */
+typedef struct ecnf_adam_opts {
+  float lr, b1, b2, eps, eps_root;
+  int32_t count;
+  float ema_beta;
+} ecnf_adam_opts;
+int ecnf_adam_update(ecnf_trainer* tr, const float* grad, float* params, float* mu, float* nu, float* ema, size_t n,
+                     const ecnf_adam_opts* opts, float* norms, void* stream);
+
+/* Replace a handle's weights with the blob `params` (on_device: a DEVICE pointer, else host).  Synchronous. */
+int ecnf_update_params(ecnf_handle* h, const float* params, int32_t on_device);
+
 /* Thread-local description of the last error ("" when none). */
 const char* ecnf_last_error(void);
 

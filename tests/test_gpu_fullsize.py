@@ -4,8 +4,8 @@ of it are checked against the fp64 oracle and bitwise against a small-batch run 
   * LJ13, B = 1024, Euler NFE = 100 (the headline workload): 6 strided molecules vs the fp64 oracle, |err| <= 1e-4
   * ALDP, B = 512 real frames of the reference's aldp_500K_train_mini.h5 (zero-CoM centred, setup_training.py:91-94),
     get_log_prob with PIDController(rtol = atol = 1e-5) and Hutchinson: 4 strided molecules held to the adaptive
-    envelope of test_gpu_parity.py (within 2x (+2e-4 / +2e-3) the fp32 oracle's own distance to an accurate fp64
-    fixed-step solution)
+    envelope of test_gpu_parity.py (within 2x (+2e-4 / +2e-3) the largest distance of the fp32 oracle's own solves
+    of x and 3 perturbed copies to an accurate fp64 fixed-step solution)
   * QM9 shape (N = 29, M = 256, L = 4, K = 5), B = 2048, Euler NFE = 10 (the full NFE-100 batch is timed by
     tools/bench_paths.py; 10 steps bound the oracle's CPU time): 2 strided molecules vs fp64, |err| <= 1e-4
 """
@@ -70,14 +70,24 @@ def test_aldp_b512_adaptive_hutchinson_log_prob():
     assert (st.cpu().numpy() == 0).all() and torch.isfinite(dl).all()
     lp = (h.base_log_prob(xb) + dl).cpu().numpy()
     idx = np.array([0, 170, 341, 511])
-    lp_32, _, dl_32, nfe_32, x_32 = O.get_log_prob(p, oc, x[idx], feat[idx], eps=eps[idx], approx=True,
-                                                    solver="dopri5", dt0=None, dtype=np.float32)
     lp_f, _, dl_f, _, x_f = O.get_log_prob(p, oc, x[idx], feat[idx], eps=eps[idx], approx=True, solver="dopri5",
                                            dt0=0.005, dtype=np.float64)
-    ek, eo = np.abs(xb.cpu().numpy()[idx] - x_f).max(), np.abs(x_32 - x_f).max()
-    assert ek <= 2 * eo + 2e-4, (ek, eo)
-    ek, eo = np.abs(lp[idx] - lp_f).max(), np.abs(lp_32 - lp_f).max()
-    assert ek <= 2 * eo + 2e-3, (ek, eo)
+    # the envelope: the oracle's own fp32 adaptive solves of x and of 3 copies perturbed by 1e-7 (relative) -- these
+    # ~900-step solves fork: the perturbations alone move one molecule's log-prob by 0.05 .. 0.34
+    eo_x = eo_lp = 0.0
+    for k in range(4):
+        xk = x[idx] if k == 0 else \
+            (x[idx] * (1 + 1e-7 * np.random.default_rng(100 + k).standard_normal(x[idx].shape))).astype(np.float32)
+        lp_32, _, _, nfe_k, x_32 = O.get_log_prob(p, oc, xk, feat[idx], eps=eps[idx], approx=True, solver="dopri5",
+                                                  dt0=None, dtype=np.float32)
+        eo_x = max(eo_x, float(np.abs(x_32 - x_f).max()))
+        eo_lp = max(eo_lp, float(np.abs(lp_32 - lp_f).max()))
+        if k == 0:
+            nfe_32 = nfe_k
+    ek = np.abs(xb.cpu().numpy()[idx] - x_f).max()
+    assert ek <= 2 * eo_x + 2e-4, (ek, eo_x)
+    ek = np.abs(lp[idx] - lp_f).max()
+    assert ek <= 2 * eo_lp + 2e-3, (ek, eo_lp)
     nfe = nfe.cpu().numpy()
     assert abs(nfe[idx].mean() - nfe_32.mean()) <= 0.3 * nfe_32.mean(), (nfe[idx], nfe_32)
     xb_s, dl_s, _, _ = h.integrate(g(x[idx]), g(feat[idx], torch.int32), 1.0, 0.0, SolveOptions("dopri5", None),

@@ -91,14 +91,19 @@ def test_jvp_is_fp32_class():
 
 
 def _overflow_case():
-    """LJ13 at the default init with molecules 1 and 3 scaled x100: their edge pre-activations reach ~1e5
-    (|r|^2 ~ 1e4 into phi_e.0), beyond fp16, while plain fp32 stays accurate (the oracle's fp32 / fp64 agree to
-    ~1e-6 of the displacement)."""
+    """LJ13 at the default init with molecule 1 scaled x1000 (edge pre-activations ~1e8, |r|^2 ~ 1e6 into phi_e.0:
+    beyond fp16 for certain) and molecule 3 x100 (~1e5: near the fp16 limit, either outcome allowed), while plain
+    fp32 stays accurate (the oracle's fp32 / fp64 agree to ~1e-6 of the displacement)."""
     cfg, oc, p, x0, feat = _inputs("lj13", 4, stress=False)
     x0 = x0.copy()
-    x0[1] *= 100.0
+    x0[1] *= 1000.0
     x0[3] *= 100.0
     return cfg, oc, p, x0, feat
+
+
+def _check_flags(st):
+    assert st[0] == 0 and st[2] == 0 and st[1] == _lib.ECNF_E_NONFINITE, st
+    assert st[3] in (0, _lib.ECNF_E_NONFINITE), st
 
 
 def test_nonfinite_status_and_fp32_fallback():
@@ -107,21 +112,25 @@ def test_nonfinite_status_and_fp32_fallback():
     opts = SolveOptions("euler", 0.5)
     y_raw, _, _, st = h.integrate(g(x0), g(feat, torch.int32), 0.0, 1.0, opts, check_status=False)
     st = st.cpu().numpy()
-    assert list(st) == [0, _lib.ECNF_E_NONFINITE, 0, _lib.ECNF_E_NONFINITE], st
-    assert torch.isfinite(y_raw[[0, 2]]).all()
+    _check_flags(st)
+    ok = st == 0
+    assert torch.isfinite(y_raw[torch.from_numpy(ok).cuda()]).all()
     # the host re-solves the flagged molecules on the strict-fp32 kernels (no CPU path)
     y, _, nfe, st2 = h.integrate(g(x0), g(feat, torch.int32), 0.0, 1.0, opts)
     assert (st2.cpu().numpy() == 0).all() and torch.isfinite(y).all()
-    assert torch.equal(y[[0, 2]], y_raw[[0, 2]])
+    assert torch.equal(y[torch.from_numpy(ok).cuda()], y_raw[torch.from_numpy(ok).cuda()])
     ref64, _ = O.sample_cnf(p, oc, x0, feat, solver="euler", dt0=0.5, dtype=np.float64)
     ref32, _ = O.sample_cnf(p, oc, x0, feat, solver="euler", dt0=0.5, dtype=np.float32)
-    disp = np.abs(ref64 - x0).max()
-    e = np.abs(y.cpu().numpy() - ref64).max()
-    assert e <= C * np.abs(ref32 - ref64).max() + 1e-6 * disp, (e, disp)
+    # molecule 1 sits at |x| ~ 1e8 after the first step, where summation order alone moves fp32 results by ~1e-5
+    # relative (the fp32 kernels: 1.8e-5, the numpy fp32 oracle: 1.7e-6): the bound is relative to |x| there
+    e = np.abs(y.cpu().numpy() - ref64).max(axis=1)
+    e32 = np.abs(ref32 - ref64).max(axis=1)
+    scale = np.abs(ref64).max(axis=1)
+    assert (e <= C * e32 + 3e-5 * scale).all(), (e, e32, scale)
     # fp32 handles directly: the same numbers, ECNF_OK
     h32 = EcnfHandle(cfg, p, 0, precision="fp32")
-    y32, _, _, st3 = h32.integrate(g(x0[[1, 3]]), g(feat[[1, 3]], torch.int32), 0.0, 1.0, opts)
-    assert torch.equal(y32, y[[1, 3]]) and (st3.cpu().numpy() == 0).all()
+    y32, _, _, st3 = h32.integrate(g(x0[[1]]), g(feat[[1]], torch.int32), 0.0, 1.0, opts)
+    assert torch.equal(y32, y[[1]]) and (st3.cpu().numpy() == 0).all()
 
 
 def test_nonfinite_in_divergence_solve():
@@ -130,15 +139,16 @@ def test_nonfinite_in_divergence_solve():
     eps = np.random.default_rng(2).standard_normal(x0.shape).astype(np.float32)
     _, dl, _, st = h.integrate(g(x0), g(feat, torch.int32), 0.0, 1.0, SolveOptions("euler", 0.5),
                                divergence=_lib.DIV_HUTCHINSON, eps=g(eps), check_status=False)
-    st = st.cpu().numpy()
-    assert st[0] == 0 and st[2] == 0 and st[1] == _lib.ECNF_E_NONFINITE and st[3] == _lib.ECNF_E_NONFINITE
+    _check_flags(st.cpu().numpy())
     x1, dl2, _, st2 = h.integrate(g(x0), g(feat, torch.int32), 0.0, 1.0, SolveOptions("euler", 0.5),
                                   divergence=_lib.DIV_HUTCHINSON, eps=g(eps))
     assert (st2.cpu().numpy() == 0).all() and torch.isfinite(dl2).all()
-    x1r, lq_ref, _ = O.sample_and_log_prob(p, oc, x0, feat, eps=eps, approx=True, solver="euler", dt0=0.5,
-                                           dtype=np.float64)
+    _, lq64, _ = O.sample_and_log_prob(p, oc, x0, feat, eps=eps, approx=True, solver="euler", dt0=0.5,
+                                       dtype=np.float64)
+    _, lq32, _ = O.sample_and_log_prob(p, oc, x0, feat, eps=eps, approx=True, solver="euler", dt0=0.5,
+                                       dtype=np.float32)
     lq = (h.base_log_prob(g(x0)) - dl2).cpu().numpy()
-    assert np.abs(lq - lq_ref).max() <= 1e-4 * max(1.0, np.abs(lq_ref).max())
+    assert np.abs(lq - lq64).max() <= C * np.abs(lq32 - lq64).max() + 1e-5 * max(1.0, np.abs(lq64).max())
 
 
 def test_device_feature_ids_checked_in_kernel():
