@@ -18,7 +18,8 @@ CHILD process, before this process touches the GPU) and exits with its status; u
 Extra fields: "roofline" (dominant kernel = integrate_kernel, MFMA bound: algorithmic fp32 FLOPs per launch /
 average launch time from HIP events on the launch stream, against the ceiling of the kernel's instruction mix —
 GEMM FLOPs at the split-fp16 rate, vector FLOPs at the fp32 rate; see roofline_peak), "matmul" (which arithmetic the
-GEMMs run, and the strict-fp32 kernels' time on the same workload), "logprob" (the eval leg) and "cpu_baseline" (a
+GEMMs run, and the strict-fp32 kernels' time on the same workload), "logprob" (the eval leg), "train" (the
+flow-matching training step at lj13.yaml's batch 64) and "cpu_baseline" (a
 torch-CPU fp32 batched restatement of the same Euler solve on a bounded sample, rank 0 at N = 1 only).
 """
 from __future__ import annotations
@@ -153,6 +154,8 @@ def main():
                     help="eval leg (sample + Hutchinson log-prob + target + ESS) passes: default 1 over several ranks, "
                          "0 at one rank")
     ap.add_argument("--fp32-steps", type=int, default=2, help="launches of the strict-fp32 kernels timed (0 = skip)")
+    ap.add_argument("--train-steps", type=int, default=10, help="timed training steps at N = 1 (0 = skip)")
+    ap.add_argument("--train-batch", type=int, default=64, help="training batch (lj13.yaml: 64)")
     ap.add_argument("--cpu-molecules", type=int, default=256, help="bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--cpu-molecules-1t", type=int, default=48, help="bounded 1-thread CPU-baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "0") or 0))
@@ -285,6 +288,35 @@ def main():
                      x1_lp=x1.cpu().numpy(), log_q=log_q.cpu().numpy(), log_w=log_w.cpu().numpy(),
                      rev_ess=float(rev), fwd_ess=float(fwd), mean_log_q=float(mean_lq), world=world)
 
+    # training leg (SURVEY 8f rank 3, lj13.yaml training: Adam, batch 64): one flow_matching_update_fn step =
+    # loss + reverse-mode gradient + Adam, on the same device (N = 1 only)
+    train = None
+    if world == 1 and args.train_steps > 0:
+        from ecnf_amd import train as TRN
+        tr = TRN.Trainer(cfg, max_batch=args.train_batch, device=local)
+        p = tr.device_params(init_params(cfg, 0))
+        mu, nu = torch.zeros_like(p), torch.zeros_like(p)
+        gtr = torch.Generator(device=dev)
+        gtr.manual_seed(5)
+        xd = h.base_sample(torch.randn((args.train_batch, cfg.event_dim), generator=gtr, device=dev))
+        xb = h.base_sample(torch.randn((args.train_batch, cfg.event_dim), generator=gtr, device=dev))
+        tt = torch.rand((args.train_batch,), generator=gtr, device=dev)
+        ft = torch.zeros((args.train_batch, cfg.n_nodes), device=dev, dtype=torch.int32)
+        for i in range(args.train_steps + 2):
+            if i == 2:
+                torch.cuda.synchronize(dev)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+            loss, grad = tr.loss_and_grad(p, xd, xb, tt, ft)
+            tr.adam_update(grad, p, mu, nu, None, lr=1e-4, count=i + 1)
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        ms = e0.elapsed_time(e1) / args.train_steps
+        train = {"workload": f"{args.config} flow-matching training step (loss + reverse-mode gradient + Adam), "
+                             f"batch {args.train_batch}, strict-fp32 MFMA GEMMs",
+                 "ms_per_step": ms, "steps_per_s": 1e3 / ms, "molecules_per_s": args.train_batch * 1e3 / ms,
+                 "loss": float(loss)}
+
     cpu = None
     if rank == 0 and world == 1 and args.cpu_molecules > 0:
         threads = args.cpu_threads or len(os.sched_getaffinity(0))
@@ -328,6 +360,7 @@ def main():
                                         "terms, vector FLOPs at the fp32 peak") if chain_mode in SPLIT_TERMS
                                        else "fp32 MFMA peak"},
             "logprob": logprob,
+            "train": train,
             "cpu_baseline": cpu,
         }
         pmc = os.path.join(ROOT, "profiles", f"pmc_traffic_{args.config}_b{B}.json")

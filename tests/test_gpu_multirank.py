@@ -22,7 +22,7 @@ if not torch.cuda.is_available():
     pytest.skip("needs a ROCm GPU", allow_module_level=True)
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-ARGS = ["--batch", "96", "--nfe", "10", "--steps", "1", "--warmup", "1", "--logprob", "1", "--fp32-steps", "0",
+ARGS = ["--batch", "96", "--nfe", "10", "--steps", "1", "--warmup", "1", "--logprob", "1", "--fp32-steps", "0", "--train-steps", "0",
         "--cpu-molecules", "0"]
 
 

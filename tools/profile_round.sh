@@ -7,7 +7,7 @@ cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 OUT="$GRAFT_REPO_ROOT/gpurun_out/prof_$TAG"
 mkdir -p "$OUT"
-B="bench.py --steps 3 --warmup 1 --cpu-molecules 0"
+B="bench.py --steps 3 --warmup 1 --cpu-molecules 0 --fp32-steps 0 --train-steps 0"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o run --output-format csv -- python3 $B > "$OUT/kt.log" 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex integrate_kernel -d "$OUT/fetch" -o run --output-format csv -- python3 $B > "$OUT/fetch.log" 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex integrate_kernel -d "$OUT/write" -o run --output-format csv -- python3 $B > "$OUT/write.log" 2>&1 || exit $?
