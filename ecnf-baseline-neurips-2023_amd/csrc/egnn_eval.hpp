@@ -1073,7 +1073,7 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
 
 // ---------------------------------------------------------------------------------------------------
 // one full evaluation.  x_in/tan_in/v_out/tan_out: LDS [MPW][N*D]; t_in: LDS [MPW] (actual time).
-// Must be called by all 256 threads; returns after a barrier.
+// Must be called by all Geo<NF, NT, P>::NTHR threads of the workgroup (NW waves); returns after a barrier.
 // ---------------------------------------------------------------------------------------------------
 template <int NF, int NT, int L, int D, int P>
 __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const float* x_in, const float* t_in, const float* tan_in,

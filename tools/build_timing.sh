@@ -11,6 +11,6 @@ for spec in "$@"; do
   fi
   /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -std=c++17 -fPIC -shared -fno-slp-vectorize -mllvm -amdgpu-mfma-vgpr-form \
     -Wno-pass-failed -Wno-unused-value -Wno-unused-result ${DEVFLAGS:--DECNF_DEV_LJ13_ONLY} $flags -I "$SRC/include" \
-    -o "$ROOT/tools/libt_${name}.so" "$SRC/ecnf-baseline-neurips-2023_amd/csrc/ecnf_hip.hip" &
+    -o "$ROOT/tools/libt_${name}.so" "$SRC/ecnf-baseline-neurips-2023_amd/csrc/ecnf_hip.hip" "$ROOT/ecnf-baseline-neurips-2023_amd/csrc/ecnf_train.hip" &
 done
 wait
