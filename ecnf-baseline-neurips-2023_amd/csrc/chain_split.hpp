@@ -90,6 +90,13 @@ __device__ __forceinline__ void split_pair(float y0, float y1, unsigned (&p)[kPi
   p[2] = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){r0, r1}, bf16x2));
 #else
   p[0] = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){y0, y1}, f16x2));
+#ifdef ECNF_SPLIT_C_RESIDUAL   // experiment: the residual in plain C (schedulable VALU, 2 more instructions per pair)
+  {
+    const f16x2 h = __builtin_bit_cast(f16x2, p[0]);
+    p[1] = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){y0 - (float)h[0], y1 - (float)h[1]}, f16x2));
+    return;
+  }
+#endif
   // p1 = fp16(y - fp16 piece 0) per half: the mixed-precision FMA reads the f16 half directly, the difference is
   // exact in fp32 and rounded once (hipcc does not form v_fma_mix from C here)
   unsigned lo;
@@ -291,28 +298,26 @@ __device__ __forceinline__ void chain_split(SplitX<NF>& XA, SplitX<NF>& XB, f32x
       constexpr int id = Plan::nth(gg + 1, 0, decltype(Kc)::value);
       bv[id] = *reinterpret_cast<const f32x2*>(lbias + Plan::bias_off(id));
     });
-    if constexpr (mfma_group) {
+    auto mfma_t = [&](auto Tc) {
+      constexpr int t = decltype(Tc)::value;
       auto& Xin = pick<l & 1>(XA, XB);
       const u32x4* A = wbuf[gg % (PF + 1)];
       const u32x4* B = Xin.v[fb][u];
       const u32x4* BT = pick<l & 1>(XAT, XBT).v[fb][u];
-      static_for<kTerms>([&](auto Tc) {
-        constexpr int t = decltype(Tc)::value;
-        constexpr int pa = term_w(t), pb = term_x(t);   // cross terms, smallest first
-        if constexpr (fb == 0 && u == 0 && t == 0) {
-          const f32x16 z = {};
+      constexpr int pa = term_w(t), pb = term_x(t);   // cross terms, smallest first
+      if constexpr (fb == 0 && u == 0 && t == 0) {
+        const f32x16 z = {};
 #ifdef ECNF_CHAIN_BIAS_INIT
-          acc[jb] = mfma_split(A[pa], B[pb], cb);
+        acc[jb] = mfma_split(A[pa], B[pb], cb);
 #else
-          acc[jb] = mfma_split(A[pa], B[pb], z);
+        acc[jb] = mfma_split(A[pa], B[pb], z);
 #endif
-          if constexpr (NT) accT[jb] = mfma_split(A[pa], BT[pb], z);
-        } else {
-          acc[jb] = mfma_split(A[pa], B[pb], acc[jb]);
-          if constexpr (NT) accT[jb] = mfma_split(A[pa], BT[pb], accT[jb]);
-        }
-      });
-    }
+        if constexpr (NT) accT[jb] = mfma_split(A[pa], BT[pb], z);
+      } else {
+        acc[jb] = mfma_split(A[pa], B[pb], acc[jb]);
+        if constexpr (NT) accT[jb] = mfma_split(A[pa], BT[pb], accT[jb]);
+      }
+    };
 #if defined(ECNF_SPLIT_CHEAP_ACT)   // timing experiment: keep the data flow (one VALU per pair), drop the arithmetic
     static_for<nC>([&](auto Kc) {
       constexpr int id = Plan::nth(gg, 2, decltype(Kc)::value);
@@ -320,13 +325,14 @@ __device__ __forceinline__ void chain_split(SplitX<NF>& XA, SplitX<NF>& XB, f32x
       constexpr int r = 2 * it.p;
       if constexpr (it.l < NL - 1) {
         auto& Xo = pick<(it.l + 1) & 1>(XA, XB);
-        Xo.v[it.j][r >> 3][0][(r & 7) >> 1] =
-            __builtin_bit_cast(unsigned, acc[it.j][r]) ^ __builtin_bit_cast(unsigned, acc[it.j][r + 1]);
+        const unsigned q = __builtin_bit_cast(unsigned, acc[it.j][r]) ^ __builtin_bit_cast(unsigned, acc[it.j][r + 1]);
+        Xo.v[it.j][r >> 3][0][(r & 7) >> 1] = q;
+        Xo.v[it.j][r >> 3][1][(r & 7) >> 1] = q;   // every piece defined: no MFMA folds away
       }
     });
 #elif !defined(ECNF_SPLIT_NO_ACT)
     // stage A
-    static_for<nA>([&](auto Kc) {
+    auto stageA = [&]() { static_for<nA>([&](auto Kc) {
       constexpr int id = Plan::nth(gg, 0, decltype(Kc)::value);
       constexpr typename Plan::Item it = Plan::item(id);
       constexpr int r = 2 * it.p;
@@ -337,8 +343,16 @@ __device__ __forceinline__ void chain_split(SplitX<NF>& XA, SplitX<NF>& XB, f32x
       uv[id][0] = fmaf(acc[it.j][r], inv.v[it.l], bv[id][0]);
       uv[id][1] = fmaf(acc[it.j][r + 1], inv.v[it.l], bv[id][1]);
 #endif
+#if defined(ECNF_SPLIT_IDENT_ACT)   // timing experiment: identity activation (split kept, SiLU arithmetic dropped)
+      ev[id][0] = 1.0f;
+      ev[id][1] = 1.0f;
+#elif defined(ECNF_SPLIT_NO_TRANS)   // timing experiment: the transcendentals replaced by plain VALU (same data flow)
+      ev[id][0] = uv[id][0] * 0.5f;
+      ev[id][1] = uv[id][1] * 0.5f;
+#else
       ev[id][0] = __builtin_amdgcn_exp2f(uv[id][0]);
       ev[id][1] = __builtin_amdgcn_exp2f(uv[id][1]);
+#endif
       if constexpr (NT) {
 #ifdef ECNF_CHAIN_BIAS_INIT
         dv[id][0] = accT[it.j][r];
@@ -348,19 +362,29 @@ __device__ __forceinline__ void chain_split(SplitX<NF>& XA, SplitX<NF>& XB, f32x
         dv[id][1] = accT[it.j][r + 1] * inv.v[it.l];
 #endif
       }
-    });
+    }); };
     // stage B
-    static_for<nB>([&](auto Kc) {
+    auto stageB = [&]() { static_for<nB>([&](auto Kc) {
       constexpr int id = Plan::nth(gg, 1, decltype(Kc)::value);
+#if defined(ECNF_SPLIT_IDENT_ACT)
+#elif defined(ECNF_SPLIT_NO_TRANS)
+      ev[id][0] = 0.25f * (1.0f + ev[id][0]);
+      ev[id][1] = 0.25f * (1.0f + ev[id][1]);
+#else
       ev[id][0] = __builtin_amdgcn_rcpf(1.0f + ev[id][0]);
       ev[id][1] = __builtin_amdgcn_rcpf(1.0f + ev[id][1]);
-    });
+#endif
+    }); };
     // stage C
-    static_for<nC>([&](auto Kc) {
+    auto stageC = [&]() { static_for<nC>([&](auto Kc) {
       constexpr int id = Plan::nth(gg, 2, decltype(Kc)::value);
       constexpr typename Plan::Item it = Plan::item(id);
+#ifdef ECNF_SPLIT_IDENT_ACT
+      const float y0 = uv[id][0], y1 = uv[id][1];
+#else
       const float y0 = uv[id][0] * ev[id][0];
       const float y1 = uv[id][1] * ev[id][1];
+#endif
       if constexpr (it.l < NL - 1) {
         put_pair<NF, it.j, 2 * it.p>(pick<(it.l + 1) & 1>(XA, XB), y0, y1);
       } else {
@@ -378,7 +402,36 @@ __device__ __forceinline__ void chain_split(SplitX<NF>& XA, SplitX<NF>& XB, f32x
           accT[it.j][2 * it.p + 1] = d1;
         }
       }
-    });
+    }); };
+#endif
+#if !defined(ECNF_SPLIT_SGB) && !defined(ECNF_SPLIT_CHEAP_ACT) && !defined(ECNF_SPLIT_NO_ACT)
+    // Emission order pinned per MFMA gap: one stage per MFMA of the group (stage C, B, A after the 1st, 2nd, 3rd
+    // MFMA term: each ~20 cycles of issue for one item, inside the 24 free issue cycles of a 32-cycle MFMA), every
+    // gap closed by a sched_barrier.  Stage C consumes the rcp of the previous group, stage A reads an accumulator
+    // finished at least one group earlier, so no gap waits on its own MFMA.  (The sched_group_barrier form,
+    // -DECNF_SPLIT_SGB, left 2/3 of the gaps empty and bunched 40-100 issue cycles into the others.)
+    if constexpr (mfma_group) {
+      __builtin_amdgcn_sched_barrier(0);
+      static_for<kTerms>([&](auto Tc) {
+        constexpr int t = decltype(Tc)::value;
+        constexpr int stage = 2 - (t * 3) / kTerms;   // C, B, A
+        mfma_t(Tc);
+        if constexpr (stage == 2) stageC();
+        if constexpr (stage == 1) stageB();
+        if constexpr (stage == 0) stageA();
+        __builtin_amdgcn_sched_barrier(0);
+      });
+    } else {
+      stageA();
+      stageB();
+      stageC();
+    }
+#else
+    if constexpr (mfma_group) static_for<kTerms>([&](auto Tc) { mfma_t(Tc); });
+#if !defined(ECNF_SPLIT_CHEAP_ACT) && !defined(ECNF_SPLIT_NO_ACT)
+    stageA();
+    stageB();
+    stageC();
 #endif
     if constexpr (mfma_group) {
       // schedule: weight loads, bias reads, then MFMA / VALU alternating
@@ -402,6 +455,7 @@ __device__ __forceinline__ void chain_split(SplitX<NF>& XA, SplitX<NF>& XB, f32x
 #endif
       __builtin_amdgcn_sched_barrier(0);
     }
+#endif
   });
   __builtin_amdgcn_s_setprio(0);
 }

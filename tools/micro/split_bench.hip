@@ -62,8 +62,8 @@ int main() {
   std::vector<float> hb(5 * M);
   for (int i = 0; i < 5 * M; ++i) hb[i] = 0.01f * (i % 7);
   unsigned* W; float *b, *out; unsigned long long* cyc;
-  (void)hipMalloc(&W, nW * 4); (void)hipMalloc(&b, 5 * M * 4); (void)hipMalloc(&out, 256 * 256 * 4);
-  (void)hipMalloc(&cyc, 256 * 4 * 8);
+  (void)hipMalloc(&W, nW * 4); (void)hipMalloc(&b, 5 * M * 4); (void)hipMalloc(&out, 256 * 64 * WAVES * 4);   // one float per thread
+  (void)hipMalloc(&cyc, 256 * WAVES * 8);   // one slot per wave
   (void)hipMemcpy(W, hw.data(), nW * 4, hipMemcpyHostToDevice);
   (void)hipMemcpy(b, hb.data(), 5 * M * 4, hipMemcpyHostToDevice);
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 120 * 1024);
