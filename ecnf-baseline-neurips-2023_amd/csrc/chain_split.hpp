@@ -178,6 +178,19 @@ struct SplitPlan {
       if (stage_g(item(i), S) == g && k-- == 0) return i;
     return -1;
   }
+  // the same restricted to items whose previous stage sits in the same group (late = true: compressed windows, which
+  // must follow that stage inside the group) or in an earlier one (late = false); S = 1, 2
+  static constexpr bool is_late(const Item& it, int S) { return stage_g(it, S - 1) == stage_g(it, S); }
+  static constexpr int count_l(int g, int S, bool late) {
+    int n = 0;
+    for (int i = 0; i < NI; ++i) n += stage_g(item(i), S) == g && is_late(item(i), S) == late;
+    return n;
+  }
+  static constexpr int nth_l(int g, int S, bool late, int k) {
+    for (int i = 0; i < NI; ++i)
+      if (stage_g(item(i), S) == g && is_late(item(i), S) == late && k-- == 0) return i;
+    return -1;
+  }
   // LDS address (floats, lane half 0) of the two biases of item id; the lane half adds 4
   static constexpr int bias_off(int id) {
     const Item it = item(id);
@@ -364,8 +377,8 @@ __device__ __forceinline__ void chain_split(SplitX<NF>& XA, SplitX<NF>& XB, f32x
       }
     }); };
     // stage B
-    auto stageB = [&]() { static_for<nB>([&](auto Kc) {
-      constexpr int id = Plan::nth(gg, 1, decltype(Kc)::value);
+    auto stageB = [&](auto Late) { static_for<Plan::count_l(gg, 1, decltype(Late)::value)>([&](auto Kc) {
+      constexpr int id = Plan::nth_l(gg, 1, decltype(Late)::value, decltype(Kc)::value);
 #if defined(ECNF_SPLIT_IDENT_ACT)
 #elif defined(ECNF_SPLIT_NO_TRANS)
       ev[id][0] = 0.25f * (1.0f + ev[id][0]);
@@ -376,8 +389,8 @@ __device__ __forceinline__ void chain_split(SplitX<NF>& XA, SplitX<NF>& XB, f32x
 #endif
     }); };
     // stage C
-    auto stageC = [&]() { static_for<nC>([&](auto Kc) {
-      constexpr int id = Plan::nth(gg, 2, decltype(Kc)::value);
+    auto stageC = [&](auto Late) { static_for<Plan::count_l(gg, 2, decltype(Late)::value)>([&](auto Kc) {
+      constexpr int id = Plan::nth_l(gg, 2, decltype(Late)::value, decltype(Kc)::value);
       constexpr typename Plan::Item it = Plan::item(id);
 #ifdef ECNF_SPLIT_IDENT_ACT
       const float y0 = uv[id][0], y1 = uv[id][1];
@@ -416,22 +429,31 @@ __device__ __forceinline__ void chain_split(SplitX<NF>& XA, SplitX<NF>& XB, f32x
         constexpr int t = decltype(Tc)::value;
         constexpr int stage = 2 - (t * 3) / kTerms;   // C, B, A
         mfma_t(Tc);
-        if constexpr (stage == 2) stageC();
-        if constexpr (stage == 1) stageB();
-        if constexpr (stage == 0) stageA();
+        // items whose windows were compressed (two stages in one group) run in A, B, C order after stage A
+        if constexpr (stage == 2) stageC(std::false_type{});
+        if constexpr (stage == 1) stageB(std::false_type{});
+        if constexpr (stage == 0) {
+          stageA();
+          stageB(std::true_type{});
+          stageC(std::true_type{});
+        }
         __builtin_amdgcn_sched_barrier(0);
       });
     } else {
       stageA();
-      stageB();
-      stageC();
+      stageB(std::false_type{});
+      stageB(std::true_type{});
+      stageC(std::false_type{});
+      stageC(std::true_type{});
     }
 #else
     if constexpr (mfma_group) static_for<kTerms>([&](auto Tc) { mfma_t(Tc); });
 #if !defined(ECNF_SPLIT_CHEAP_ACT) && !defined(ECNF_SPLIT_NO_ACT)
     stageA();
-    stageB();
-    stageC();
+    stageB(std::false_type{});
+    stageB(std::true_type{});
+    stageC(std::false_type{});
+    stageC(std::true_type{});
 #endif
     if constexpr (mfma_group) {
       // schedule: weight loads, bias reads, then MFMA / VALU alternating
@@ -485,6 +507,127 @@ __device__ __forceinline__ void chain_split_tangent(f32x16 (&X)[NF], f32x16 (&XT
     });
   });
   chain_split<NF, NL, 1>(XA, XB, X, Wpk, bias, inv, lane, XAT, XBT, XT);
+#pragma unroll
+  for (int fb = 0; fb < NF; ++fb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      X[fb][r] *= kNegLn2;
+      XT[fb][r] *= kNegLn2;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------------
+// M = 256 tangent kernels (QM9): the forward-mode edge chain with the primal and the tangent in SEQUENTIAL passes
+// per layer.  chain_split_tangent interleaves both on every weight fragment, which needs split input + output
+// buffers and accumulators for both (6 x 128 registers at NF = 8); here a layer is
+//   1. primal pass:  acc  = b' + W X'    (X' split block by block into XA just before its first k-step is needed;
+//                                         the accumulators start at the log2-domain bias column)
+//   2. tangent pass: accT = W X'_T      (the same fragments streamed again)
+//   3. activation:   X'  = u / (1 + 2^u),  X'_T = r (1 - ln2 u (1 - r)) du   (u = acc, du = accT, r = 1/(1+2^u))
+// so at most acc + XAT + accT (3 x 128 registers) are live.  X, XT: the log2-domain activations in fp32
+// accumulator layout (in_log2 = false: natural-domain input, scaled by -log2 e first); on return the natural-domain
+// output (x -ln 2).  Weights: the primal chain's split fragments [layer][group (jb, fb, u)][piece][lane].
+// ---------------------------------------------------------------------------------------------------
+template <int NF>
+__device__ __forceinline__ void split_blocks(const f32x16 (&X)[NF], SplitX<NF>& S) {
+  static_for<NF>([&](auto Fc) {
+    constexpr int fb = decltype(Fc)::value;
+    static_for<8>([&](auto Ic) {
+      constexpr int i = decltype(Ic)::value;
+      put_pair<NF, fb, 2 * i>(S, X[fb][2 * i], X[fb][2 * i + 1]);
+    });
+  });
+}
+
+// one pass of one layer: acc[jb] = (BIAS ? b' : 0) + sum over (fb, u) of W[l][jb][fb][u] X'[fb][u]
+template <int NF, bool BIAS>
+__device__ __forceinline__ void dual_pass(const SplitX<NF>& X, f32x16 (&acc)[NF], __amdgpu_buffer_rsrc_t rsrc,
+                                          int voff, int layer_soff, const float* __restrict__ lbias) {
+  constexpr int G = 2 * NF * NF, PF = ECNF_SPLIT_PF;
+  u32x4 wbuf[PF + 1][kPieces];
+  static_for<PF>([&](auto Gc) {
+    constexpr int gg = decltype(Gc)::value;
+#pragma unroll
+    for (int p = 0; p < kPieces; ++p) wbuf[gg][p] = wload(rsrc, voff, layer_soff + (gg * kPieces + p) * kPieceBytes);
+  });
+  static_for<G>([&](auto Gc) {
+    constexpr int gg = decltype(Gc)::value;
+    constexpr int jb = gg / (2 * NF), fb = (gg % (2 * NF)) >> 1, u = gg & 1;
+    if constexpr (gg + PF < G) {
+#pragma unroll
+      for (int p = 0; p < kPieces; ++p)
+        wbuf[(gg + PF) % (PF + 1)][p] = wload(rsrc, voff, layer_soff + ((gg + PF) * kPieces + p) * kPieceBytes);
+    }
+    if constexpr (fb == 0 && u == 0) {
+      if constexpr (BIAS) {
+        f32x16 c;
+        static_for<4>([&](auto Qc) {
+          constexpr int q = decltype(Qc)::value;
+          const f32x4 b4 = *reinterpret_cast<const f32x4*>(lbias + jb * 32 + 8 * q);
+          c[4 * q] = b4[0];
+          c[4 * q + 1] = b4[1];
+          c[4 * q + 2] = b4[2];
+          c[4 * q + 3] = b4[3];
+        });
+        acc[jb] = c;
+      } else {
+        acc[jb] = f32x16{};
+      }
+    }
+    const u32x4* A = wbuf[gg % (PF + 1)];
+    static_for<kTerms>([&](auto Tc) {
+      constexpr int t = decltype(Tc)::value;
+      acc[jb] = mfma_split(A[term_w(t)], X.v[fb][u][term_x(t)], acc[jb]);
+    });
+    __builtin_amdgcn_sched_barrier(0);
+  });
+}
+
+template <int NF, int NL>
+__device__ __forceinline__ void chain_dual_seq(f32x16 (&X)[NF], f32x16 (&XT)[NF], const unsigned* __restrict__ Wpk,
+                                               const float* __restrict__ bias, int lane, bool in_log2) {
+  constexpr float kNegLog2e = -1.4426950408889634f, kNegLn2 = -0.69314718055994531f;
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned*>(Wpk), (short)0,
+                                                                         0x7fffffff, 0x00020000);
+  const int voff = lane * 16;
+  const float* lbias = bias + 4 * (lane >> 5);
+  if (!in_log2) {
+#pragma unroll
+    for (int fb = 0; fb < NF; ++fb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        X[fb][r] *= kNegLog2e;
+        XT[fb][r] *= kNegLog2e;
+      }
+  }
+  // a runtime layer loop with scheduling fences between the phases: only one pass's operands are live at a time
+  for (int l = 0; l < NL; ++l) {
+    const int soff = l * (2 * NF * NF) * kPieces * kPieceBytes;
+    {
+      SplitX<NF> XA;
+      split_blocks<NF>(X, XA);
+      __builtin_amdgcn_sched_barrier(0);
+      dual_pass<NF, true>(XA, X, rsrc, voff, soff, lbias + l * NF * 32);   // X <- u (primal pre-activation)
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    {
+      SplitX<NF> XAT;
+      split_blocks<NF>(XT, XAT);
+      __builtin_amdgcn_sched_barrier(0);
+      dual_pass<NF, false>(XAT, XT, rsrc, voff, soff, nullptr);           // XT <- du
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int fb = 0; fb < NF; ++fb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float u = X[fb][r];
+        const float rr = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(u));
+        X[fb][r] = u * rr;
+        XT[fb][r] = rr * fmaf(u * (1.0f - rr), kNegLn2, 1.0f) * XT[fb][r];
+      }
+    __builtin_amdgcn_sched_barrier(0);
+  }
 #pragma unroll
   for (int fb = 0; fb < NF; ++fb)
 #pragma unroll

@@ -26,13 +26,14 @@ namespace ecnf {
   ECNF_INST_SHAPE(ECNF_INST_KW, m, l, d, 0, 0) ECNF_INST_SHAPE(ECNF_INST_KW, m, l, d, 0, 1)
 #define ECNF_INST_BOTH(m, l, d) \
   ECNF_INST_PRIMAL(m, l, d) ECNF_INST_SHAPE(ECNF_INST_KW, m, l, d, 1, 0) ECNF_INST_SHAPE(ECNF_INST_KW, m, l, d, 1, 1)
+#define ECNF_INST_WIDE(m, l, d) ECNF_INST_PRIMAL(m, l, d) ECNF_INST_SHAPE(ECNF_INST_KW, m, l, d, 1, 0)
 #ifdef ECNF_SPLIT_TU
 #define ECNF_INST_KW extern template
 #else
 #define ECNF_INST_KW template
 #endif
 ECNF_SHAPES(ECNF_INST_BOTH)
-ECNF_SHAPES_PRIMAL_ONLY(ECNF_INST_PRIMAL)
+ECNF_SHAPES_WIDE_TAN(ECNF_INST_WIDE)
 #undef ECNF_INST_KW
 
 // x0 = s * (z - mean_nodes z)   (zero_com_base.py:88-93, build_cnf.py:46)
@@ -357,6 +358,17 @@ bool split_primal(const ecnf_cfg& c, int NT, int P) {
   return kSplitChain && P == 0 && !NT && c.mlp_width <= 32 * kSplitMaxNF;
 }
 
+// Geo<NF, 1, 0>::kWideT: the M = 256 tangent kernels (per-edge phi_e.0, no P rows in LDS, in-place phi_h for one
+// 32-row node tile)
+bool wide_tangent(const ecnf_cfg& c, int NT, int P) { return NT && P == 0 && c.mlp_width == 256; }
+
+// Geo<NF, NT, P>::kSplitN: split node GEMMs, i.e. 16-B node-row strides (split primal kernels and, with
+// kSplitTanNode, the split tangent kernels)
+bool vec_layout(const ecnf_cfg& c, int NT, int P) {
+  return split_primal(c, NT, P) || (kSplitTanNode && kSplitTanChain && P == 0 && NT && c.mlp_width == 128) ||
+         wide_tangent(c, NT, P);
+}
+
 int choose_mpw(const ecnf_cfg& c, int NT, int P, int* mpw_out, size_t* lds_out, int* rp_out) {
   const int N = c.n_nodes, D = c.dim, H = c.hidden, T = c.time_embedding_dim, M = c.mlp_width;
   const int E = N * (N - 1);
@@ -368,8 +380,10 @@ int choose_mpw(const ecnf_cfg& c, int NT, int P, int* mpw_out, size_t* lds_out, 
   int best_rp = 0;
   for (int m = 1; m <= 32; ++m) {
     const int RP = 32 * ((m * N + 31) / 32);
-    const bool vec = split_primal(c, NT, P);
-    const int floats = (NT ? lds_eval_floats<1>(N, D, H, T, M, m, RP, vec) : lds_eval_floats<0>(N, D, H, T, M, m, RP, vec)) +
+    const bool vec = vec_layout(c, NT, P), wide = wide_tangent(c, NT, P);
+    if (wide && RP != 32) break;   // in-place phi_h: one 32-row node tile (node_gemm_inplace)
+    const int floats = (NT ? lds_eval_floats<1>(N, D, H, T, M, m, RP, vec, wide)
+                           : lds_eval_floats<0>(N, D, H, T, M, m, RP, vec)) +
                        solver_lds_floats(m, N * D);
     const size_t bytes = (size_t)floats * 4;
     if (bytes > 160 * 1024) break;
@@ -391,19 +405,20 @@ int choose_mpw(const ecnf_cfg& c, int NT, int P, int* mpw_out, size_t* lds_out, 
   return ECNF_OK;
 }
 
-bool shape_supported(const ecnf_cfg& c, int NT) {
+// a kernel is compiled for (cfg, NT, P); P < 0: either precision
+bool shape_supported(const ecnf_cfg& c, int NT, int P = -1) {
   const int M = c.mlp_width, L = c.mlp_depth, D = c.dim;
 #define X(m, l, d) \
   if (M == m && L == l && D == d) return true;
   ECNF_SHAPES(X)
 #undef X
-  if (NT) return false;
 #define X(m, l, d) \
-  if (M == m && L == l && D == d) return true;
-  ECNF_SHAPES_PRIMAL_ONLY(X)
+  if (M == m && L == l && D == d) return !NT || P <= 0;
+  ECNF_SHAPES_WIDE_TAN(X)
 #undef X
   return false;
 }
+
 
 hipError_t dispatch_integrate(const ecnf_handle* h, int NT, const SolveP& sp, const float* y0, const int32_t* feat,
                               const float* eps, float* y1, float* dlogp, int32_t* nfe, int32_t* status, int B,
@@ -416,9 +431,10 @@ hipError_t dispatch_integrate(const ecnf_handle* h, int NT, const SolveP& sp, co
     return NT ? (P ? ECNF_CALL(m, l, d, 1, 1) : ECNF_CALL(m, l, d, 1, 0)) : (P ? ECNF_CALL(m, l, d, 0, 1) : ECNF_CALL(m, l, d, 0, 0));
   ECNF_SHAPES(X)
 #undef X
-#define X(m, l, d) \
-  if (M == m && L == l && D == d && !NT) return P ? ECNF_CALL(m, l, d, 0, 1) : ECNF_CALL(m, l, d, 0, 0);
-  ECNF_SHAPES_PRIMAL_ONLY(X)
+#define X(m, l, d)                                                                                            \
+  if (M == m && L == l && D == d)                                                                             \
+    return NT ? (P ? hipErrorInvalidValue : ECNF_CALL(m, l, d, 1, 0)) : (P ? ECNF_CALL(m, l, d, 0, 1) : ECNF_CALL(m, l, d, 0, 0));
+  ECNF_SHAPES_WIDE_TAN(X)
 #undef X
 #undef ECNF_CALL
   return hipErrorInvalidValue;
@@ -434,9 +450,10 @@ hipError_t dispatch_vf(const ecnf_handle* h, int NT, const float* x, const float
     return NT ? (P ? ECNF_CALL(m, l, d, 1, 1) : ECNF_CALL(m, l, d, 1, 0)) : (P ? ECNF_CALL(m, l, d, 0, 1) : ECNF_CALL(m, l, d, 0, 0));
   ECNF_SHAPES(X)
 #undef X
-#define X(m, l, d) \
-  if (M == m && L == l && D == d && !NT) return P ? ECNF_CALL(m, l, d, 0, 1) : ECNF_CALL(m, l, d, 0, 0);
-  ECNF_SHAPES_PRIMAL_ONLY(X)
+#define X(m, l, d)                                                                                            \
+  if (M == m && L == l && D == d)                                                                             \
+    return NT ? (P ? hipErrorInvalidValue : ECNF_CALL(m, l, d, 1, 0)) : (P ? ECNF_CALL(m, l, d, 0, 1) : ECNF_CALL(m, l, d, 0, 0));
+  ECNF_SHAPES_WIDE_TAN(X)
 #undef X
 #undef ECNF_CALL
   return hipErrorInvalidValue;
@@ -517,8 +534,8 @@ int ecnf_create(const ecnf_cfg* cfg, const float* params, size_t n_floats, int d
   Packer pk;
   struct Off {
     size_t Wn, bn, Wp, bp, wd, We, Ws, be, wx, wg, Wh[kMaxPhiH], bh[kMaxPhiH], Wn_s, Wp_s, Wh_s[kMaxPhiH];
-    size_t bp_u, wd_u, be_u, wg_u, wx_u;
-    float bx, bg;
+    size_t bp_u, wd_u, be_u, wg_u, wx_u, Wp_sn, Wh_sn0, W1_s;
+    float bx, bg, pinv_n, hinv_n0, w1inv;
     float cinv[2 * 4 - 1], ninv, pinv, hinv[kMaxPhiH];
   };
   // packs W [K][NOUT] as split node fragments; returns the offset, *inv = 1 / its scale
@@ -553,6 +570,9 @@ int ecnf_create(const ecnf_cfg* cfg, const float* params, size_t n_floats, int d
     };
     const std::vector<float> wp_u = scaled(wp.data(), wp.size(), kNegLog2e);
     o.Wp_s = put_split_node(wp_u.data(), H, 2 * M, &o.pinv);
+    o.Wp_sn = put_split_node(wp.data(), H, 2 * M, &o.pinv_n);   // natural domain (tangent kernels)
+    // the M = 256 tangent kernels' per-edge phi_e.0: [h_s | h_r | |r|^2] rows 0 .. 2H of the kernel, x -log2(e)
+    o.W1_s = put_split_node(scaled(b.ek[0], (size_t)(2 * H + 1) * M, kNegLog2e).data(), 2 * H + 1, M, &o.w1inv);
     o.bp_u = pk.put(scaled(bp.data(), bp.size(), kNegLog2e).data(), bp.size());
     o.wd_u = pk.put(scaled(wd.data(), wd.size(), kNegLog2e).data(), wd.size());
     o.bp = pk.put(bp.data(), bp.size());
@@ -615,6 +635,7 @@ int ecnf_create(const ecnf_cfg* cfg, const float* params, size_t n_floats, int d
         const float f = kNegLn2 / std::sqrt((float)(c.n_nodes - 1));
         for (size_t i = 0; i < (size_t)M * out_f; ++i) w0[i] *= f;
         o.Wh_s[l] = put_split_node(w0.data(), in_f, out_f, &o.hinv[l]);
+        o.Wh_sn0 = put_split_node(b.hk[0], in_f, out_f, &o.hinv_n0);   // natural domain (tangent kernels)
       } else {
         o.Wh_s[l] = put_split_node(b.hk[l], in_f, out_f, &o.hinv[l]);
       }
@@ -670,10 +691,16 @@ int ecnf_create(const ecnf_cfg* cfg, const float* params, size_t n_floats, int d
       w.pinv = o.pinv;
       for (int l = 0; l <= L; ++l) w.hinv[l] = o.hinv[l];
       w.Wp_s = reinterpret_cast<const unsigned*>(dbuf + o.Wp_s);
+      w.Wp_sn = reinterpret_cast<const unsigned*>(dbuf + o.Wp_sn);
+      w.Wh_sn0 = reinterpret_cast<const unsigned*>(dbuf + o.Wh_sn0);
+      w.pinv_n = o.pinv_n;
+      w.hinv_n0 = o.hinv_n0;
+      w.W1_s = reinterpret_cast<const unsigned*>(dbuf + o.W1_s);
+      w.w1inv = o.w1inv;
     }
     int mpw = 0, rp = 0;
     size_t lds = 0;
-    if (shape_supported(c, NT) && choose_mpw(c, NT, P, &mpw, &lds, &rp) == ECNF_OK) {
+    if (shape_supported(c, NT, P) && choose_mpw(c, NT, P, &mpw, &lds, &rp) == ECNF_OK) {
       n.MPW = mpw;
       n.RP = rp;
       // split kernels store segment parts; the continuation rows [MPW][EP/32][ld_m] overlay hin (egnn_eval.hpp)
@@ -762,7 +789,8 @@ int ecnf_get_precision(ecnf_handle* h, int32_t* precision) {
 int ecnf_chain_arithmetic(ecnf_handle* h, int32_t with_tangent, int32_t* mode) {
   if (!h || !mode) return fail(ECNF_E_INVALID, "NULL argument");
   const bool split = split_primal(h->cfg, with_tangent ? 1 : 0, h->prec) ||
-                     (kSplitTanChain && h->prec == ECNF_PREC_SPLIT_F16 && with_tangent && h->cfg.mlp_width <= 128);
+                     (kSplitTanChain && h->prec == ECNF_PREC_SPLIT_F16 && with_tangent && h->cfg.mlp_width <= 128) ||
+                     (kSplitTanChain && wide_tangent(h->cfg, with_tangent ? 1 : 0, h->prec));
 #ifdef ECNF_SPLIT_BF16
   *mode = split ? ECNF_CHAIN_SPLIT_BF16 : ECNF_CHAIN_FP32_MFMA;
 #else

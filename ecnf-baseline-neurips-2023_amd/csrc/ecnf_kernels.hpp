@@ -141,7 +141,7 @@ __global__ __launch_bounds__((Geo<NF, NT, P>::NTHR)) void integrate_kernel(Net n
   constexpr int kThreads = Geo<NF, NT, P>::NTHR;
   extern __shared__ float smem[];
   const int tid = threadIdx.x, MPW = net.MPW, ND = net.ND, N = net.N;
-  const Lds s = carve_lds<NT, Geo<NF, NT, P>::kSplit>(net, smem);
+  const Lds s = carve_lds<NT, Geo<NF, NT, P>::kSplitN, Geo<NF, NT, P>::kWideT>(net, smem);
   const SolverLds st = carve_solver(s.tail, MPW, ND);
   const int mol0 = blockIdx.x * MPW;
   const int nmol = min(MPW, B - mol0);
@@ -391,7 +391,7 @@ __global__ __launch_bounds__((Geo<NF, NT, P>::NTHR)) void vf_kernel(Net net, con
   constexpr int kThreads = Geo<NF, NT, P>::NTHR;
   extern __shared__ float smem[];
   const int tid = threadIdx.x, MPW = net.MPW, ND = net.ND, N = net.N;
-  const Lds s = carve_lds<NT, Geo<NF, NT, P>::kSplit>(net, smem);
+  const Lds s = carve_lds<NT, Geo<NF, NT, P>::kSplitN, Geo<NF, NT, P>::kWideT>(net, smem);
   const SolverLds st = carve_solver(s.tail, MPW, ND);
   const int mol0 = blockIdx.x * MPW;
   const int nmol = min(MPW, B - mol0);
@@ -454,12 +454,15 @@ hipError_t launch_vf(const Net& net, size_t lds, const float* x, const float* t,
 
 // compiled shapes: (M, L, D) with tangent support where registers allow (M <= 128).  __graft_entry__.build()
 // reads these two lists to compile one ecnf_part.hip translation unit per shape.
+// ECNF_SHAPES: primal and tangent kernels in both GEMM arithmetics; ECNF_SHAPES_WIDE_TAN (M = 256): primal kernels in
+// both, tangent kernels in split fp16 only (Geo::kWideT; the strict-fp32 tangent chain needs 4 x 128 accumulator
+// registers per tile beside its inputs)
 #ifdef ECNF_DEV_LJ13_ONLY   // experiment builds (tools/build_variants.sh): the LJ13 shape only
 #define ECNF_SHAPES(X) X(128, 3, 3)
-#define ECNF_SHAPES_PRIMAL_ONLY(X)
+#define ECNF_SHAPES_WIDE_TAN(X)
 #elif defined(ECNF_DEV_M)       // experiment builds of one other shape (tools/build_timing.sh with DEVFLAGS)
 #define ECNF_SHAPES(X) X(ECNF_DEV_M, ECNF_DEV_L, ECNF_DEV_D)
-#define ECNF_SHAPES_PRIMAL_ONLY(X)
+#define ECNF_SHAPES_WIDE_TAN(X)
 #else
 #define ECNF_SHAPES(X)  \
   X(128, 3, 3)          \
@@ -471,8 +474,8 @@ hipError_t launch_vf(const Net& net, size_t lds, const float* x, const float* t,
   X(64, 3, 3)           \
   X(64, 3, 2)
 
-#define ECNF_SHAPES_PRIMAL_ONLY(X) \
-  X(256, 4, 3)                     \
+#define ECNF_SHAPES_WIDE_TAN(X) \
+  X(256, 4, 3)                  \
   X(256, 3, 3)
 #endif
 

@@ -52,6 +52,13 @@ constexpr bool kSplitTanChain = kSplitChain;
 #define ECNF_SPLIT_MAX_NF 8
 #endif
 constexpr int kSplitMaxNF = ECNF_SPLIT_MAX_NF;   // split chain up to M = 32 kSplitMaxNF
+// Tangent kernels' node GEMMs (node Dense, the phi_e.0 halves, phi_h) on the split path; -DECNF_FP32_TANGENT_NODE
+// keeps them on v_mfma_f32_32x32x2_f32.
+#ifdef ECNF_FP32_TANGENT_NODE
+constexpr bool kSplitTanNode = false;
+#else
+constexpr bool kSplitTanNode = true;
+#endif
 // P: GEMM arithmetic of the kernel.  P = 0 (ECNF_PREC_SPLIT_F16, the default) as described above; P = 1
 // (ECNF_PREC_FP32, ecnf_set_precision) every GEMM on v_mfma_f32_32x32x2_f32 with fp32 operands: the strict-fp32
 // comparator and the fallback for molecules whose activations leave the fp16 range (ECNF_E_NONFINITE).
@@ -60,6 +67,14 @@ struct Geo {
   static constexpr bool kSplit = kSplitChain && P == 0 && NT == 0 && NF <= kSplitMaxNF;
   // tangent kernels: the edge chains run split (chain_split_tangent); node GEMMs, layer 1 and the tail stay fp32
   static constexpr bool kSplitT = kSplitTanChain && P == 0 && NT == 1 && NF <= 4;
+  // node GEMMs on the split path with 16-B node-row strides: the split primal kernels and (kSplitTanNode) the
+  // M = 128 tangent kernels (the natural-domain fragment copies Wp_sn / Wh_sn0; tangent rows share every A
+  // fragment).  M = 64 (ALDP) keeps fp32 node GEMMs: the padded 16-B strides would halve its molecules per
+  // workgroup (2 -> 1; Hutchinson log_prob 55.9 -> 62.0 ms measured)
+  // M = 256 tangent kernels (QM9): per-edge phi_e.0 (no P buffer), sequential primal / tangent split chains
+  // (chain_dual_seq), phi_h in place on macc
+  static constexpr bool kWideT = kSplitTanChain && P == 0 && NT == 1 && NF == 8;
+  static constexpr bool kSplitN = kSplit || (kSplitTanNode && kSplitT && NF == 4) || kWideT;
 #ifndef ECNF_SPLIT_NW
 #define ECNF_SPLIT_NW 8
 #endif
@@ -110,6 +125,13 @@ struct BlockW {
   // 1 / the power-of-two scale of each split weight matrix (chain_split.hpp): chain layers, Wn, Wp, phi_h
   float cinv[2 * 4 - 1];
   float ninv, pinv, hinv[kMaxPhiH];
+  // natural-domain split fragments for the tangent kernels' P GEMM and phi_h.0 (the primal copies above carry the
+  // log2-domain factors), with their 1 / scale
+  const unsigned* Wp_sn; const unsigned* Wh_sn0;
+  float pinv_n, hinv_n0;
+  // M = 256 tangent kernels: phi_e.0 kernel [(2H+1)][M] x -log2(e) as split node fragments (edge_layer1_dual)
+  const unsigned* W1_s;
+  float w1inv;
 };
 
 struct Net {
@@ -200,12 +222,13 @@ __host__ __device__ inline int ld_node(int k, int odd_pad, bool vec) {
 }
 
 template <int NT>
-__host__ __device__ inline int lds_eval_floats(int N, int D, int H, int T, int M, int MPW, int RP, bool vec) {
+__host__ __device__ inline int lds_eval_floats(int N, int D, int H, int T, int M, int MPW, int RP, bool vec,
+                                               bool noP = false) {
   const int R = RP * (1 + NT);
   int n = 0;
   n += align4(R * ld_node(H + T, 1, vec));
   n += align4(R * ld_node(H, 1, vec));
-  n += align4(R * ld_node(2 * M, 3, vec));
+  if (!noP) n += align4(R * ld_node(2 * M, 3, vec));
   n += align4(R * ld_node(M, 1, vec));
   n += 3 * align4(R * D);
   n += align4(2 * MPW * D);
@@ -218,14 +241,16 @@ __host__ __device__ inline int lds_eval_floats(int N, int D, int H, int T, int M
   return n;
 }
 
-template <int NT, bool VEC>
+template <int NT, bool VEC, bool NOP = false>
 __device__ inline Lds carve_lds(const Net& net, float* base) {
   Lds s;
   const int R = net.RP * (1 + NT);
   float* p = base;
   s.hin = p;  s.ld_hin = ld_node(net.H + net.T, 1, VEC); p += align4(R * s.ld_hin);
   s.hb = p;   s.ld_hb = ld_node(net.H, 1, VEC);          p += align4(R * s.ld_hb);
-  s.P = p;    s.ld_P = ld_node(2 * net.M, 3, VEC);       p += align4(R * s.ld_P);
+  s.P = NOP ? nullptr : p;
+  s.ld_P = ld_node(2 * net.M, 3, VEC);
+  if (!NOP) p += align4(R * s.ld_P);
   s.macc = p; s.ld_m = ld_node(net.M, 1, VEC);           p += align4(R * s.ld_m);
   s.xc = p;    p += align4(R * net.D);
   s.xc0 = p;   p += align4(R * net.D);
@@ -417,15 +442,18 @@ __device__ __forceinline__ void node_task(const float* X1, int ldx1, int K1, con
   node_epilogue<NT, NA>(acc, accT, act, resid, ldr, Y, ldy, RP, nvalid, jb, n, kk);
 }
 
-// split-bf16 node GEMM task (primal only): acc[a] = b + sum_k W[k][(jb + a) * 32 + i] X[n][k], the fp32 operands
-// split into three bf16 pieces (six cross terms, chain_split.hpp).  A: host-packed fragments, K zero-padded to
-// a multiple of 16, fetched by buffer loads one k-step ahead; B: the lane's node row, 8 consecutive features
-// from LDS (odd row strides: conflict-free), split in registers; NA output blocks share every B split.
-template <int NA>
+// split node GEMM task: acc[a] = b + sum_k W[k][(jb + a) * 32 + i] X[n][k], the fp32 operands split into two fp16
+// pieces (three cross terms, chain_split.hpp).  A: host-packed fragments, K zero-padded to a multiple of 16, fetched
+// by buffer loads PFA k-steps ahead; B: the lane's node row, 8 consecutive features from LDS (16-B row strides),
+// split in registers; NA output blocks share every B split.  NT = 1 (the divergence kernels): the tangent row RP + n
+// shares every A fragment and gets no bias, act'(pre) * (X_T W) (as node_task).
+// INPLACE (Y may alias X1): every wave of the workgroup calls it once (active = false: no task) and the outputs are
+// written after a barrier that follows every wave's k-loop.
+template <int NA, int NT = 0, bool INPLACE = false>
 __device__ __forceinline__ void node_task_split(const float* X1, int ldx1, int K1, const float* X2, int ldx2, int K2,
                                                 const unsigned* __restrict__ Wpk, float winv,
                                                 const float* __restrict__ bias, bool act, const float* resid, int ldr, float* Y, int ldy, int RP,
-                                                int nvalid, int jb, int ct, int lane) {
+                                                int nvalid, int jb, int ct, int lane, bool active = true) {
 #ifndef ECNF_NODE_PFA
 #define ECNF_NODE_PFA 2
 #endif
@@ -444,13 +472,17 @@ __device__ __forceinline__ void node_task_split(const float* X1, int ldx1, int K
       bq[a][q] = bias ? gptr4(bias + (jb + a) * 32 + 8 * q + 4 * kk)[0] : f32x4{0.f, 0.f, 0.f, 0.f};
   f32x16 acc[NA], accT[NA];
 #pragma unroll
-  for (int a = 0; a < NA; ++a) acc[a] = f32x16{};
+  for (int a = 0; a < NA; ++a) {
+    acc[a] = f32x16{};
+    if constexpr (NT) accT[a] = f32x16{};
+  }
   const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned*>(Wpk), (short)0,
                                                                          0x7fffffff, 0x00020000);
   const int voff = lane * 16;
-  auto bload = [&](int ks, float (&v)[8]) {
+  // B: 8 consecutive features of node row `row` for k-step ks
+  auto bload = [&](int ks, int row, float (&v)[8]) {
     const bool first = ks < nks1;
-    const float* src = first ? X1 + n * ldx1 : X2 + n * ldx2;
+    const float* src = first ? X1 + row * ldx1 : X2 + row * ldx2;
     const int c0 = 16 * (first ? ks : ks - nks1) + 8 * kk;
     const int K = first ? K1 : K2;
     if (c0 + 8 <= K) {   // 16-B aligned (ld_node with VEC): two ds_read_b128
@@ -472,32 +504,40 @@ __device__ __forceinline__ void node_task_split(const float* X1, int ldx1, int K
 #pragma unroll
       for (int p = 0; p < kPieces; ++p) w[a][p] = wload(rsrc, voff, (((jb + a) * nks + ks) * kPieces + p) * kPieceBytes);
   };
+  auto bsplit = [&](const float (&v)[8], u32x4 (&B)[kPieces]) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      unsigned pc[kPieces];
+      split_pair(v[2 * e], v[2 * e + 1], pc);
+#pragma unroll
+      for (int p = 0; p < kPieces; ++p) B[p][e] = pc[p];
+    }
+  };
   // A fragments: a ring of S = PFA + 1 k-step slots; the load of k-step ks + PFA is issued (clamped to the last
   // k-step, so the main loop has no branches) before the MFMAs of k-step ks and pinned there by a sched_barrier,
   // so PFA k-steps of MFMAs cover its latency
   constexpr int S = PFA + 1;
-  float bv[8];
+  float bv[8], bvT[8];
   u32x4 wa[S][NA][kPieces];
-  bload(0, bv);
+  if (active) {
+  bload(0, n, bv);
+  if constexpr (NT) bload(0, RP + n, bvT);
   static_for<PFA>([&](auto Ic) { aload(min((int)decltype(Ic)::value, nks - 1), wa[decltype(Ic)::value]); });
   auto kstep = [&](int ks, auto Ic) {
     constexpr int i = decltype(Ic)::value;
     aload(min(ks + PFA, nks - 1), wa[(i + PFA) % S]);
-    u32x4 B[kPieces];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      unsigned pc[kPieces];
-      split_pair(bv[2 * e], bv[2 * e + 1], pc);
-#pragma unroll
-      for (int p = 0; p < kPieces; ++p) B[p][e] = pc[p];
-    }
-    bload(min(ks + 1, nks - 1), bv);
+    u32x4 B[kPieces], BT[kPieces];
+    bsplit(bv, B);
+    if constexpr (NT) bsplit(bvT, BT);
+    bload(min(ks + 1, nks - 1), n, bv);
+    if constexpr (NT) bload(min(ks + 1, nks - 1), RP + n, bvT);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int a = 0; a < NA; ++a)
       static_for<kTerms>([&](auto Tc) {
         constexpr int t = decltype(Tc)::value;
         acc[a] = mfma_split(wa[i][a][term_w(t)], B[term_x(t)], acc[a]);
+        if constexpr (NT) accT[a] = mfma_split(wa[i][a][term_w(t)], BT[term_x(t)], accT[a]);
       });
     __builtin_amdgcn_sched_barrier(0);
   };
@@ -509,22 +549,43 @@ __device__ __forceinline__ void node_task_split(const float* X1, int ldx1, int K
 #pragma unroll
   for (int a = 0; a < NA; ++a)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[a][r] = fmaf(acc[a][r], winv, bq[a][r >> 2][r & 3]);
+    for (int r = 0; r < 16; ++r) {
+      acc[a][r] = fmaf(acc[a][r], winv, bq[a][r >> 2][r & 3]);
+      if constexpr (NT) accT[a][r] *= winv;
+    }
+  }  // active
+  if constexpr (INPLACE) __syncthreads();
   // epilogue with 16-B LDS accesses: registers 4q..4q+3 are 4 consecutive output features
-  if (n < nvalid) {
+  if (active && n < nvalid) {
 #pragma unroll
     for (int a = 0; a < NA; ++a)
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int j = (jb + a) * 32 + 8 * q + 4 * kk;
-        f32x4 y;
+        f32x4 y, yT;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const float t = acc[a][4 * q + e];
-          y[e] = act ? t * sigmoidf_(t) : t;
+          if constexpr (NT) {
+            if (act) {
+              float ye, yte;
+              silu_dual<NT>(t, accT[a][4 * q + e], ye, yte);
+              y[e] = ye;
+              yT[e] = yte;
+            } else {
+              y[e] = t;
+              yT[e] = accT[a][4 * q + e];
+            }
+          } else {
+            y[e] = act ? t * sigmoidf_(t) : t;
+          }
         }
-        if (resid) y += *reinterpret_cast<const f32x4*>(resid + n * ldr + j);
+        if (resid) {
+          y += *reinterpret_cast<const f32x4*>(resid + n * ldr + j);
+          if constexpr (NT) yT += *reinterpret_cast<const f32x4*>(resid + (RP + n) * ldr + j);
+        }
         *reinterpret_cast<f32x4*>(Y + n * ldy + j) = y;
+        if constexpr (NT) *reinterpret_cast<f32x4*>(Y + (RP + n) * ldy + j) = yT;
       }
   }
 }
@@ -544,12 +605,12 @@ __device__ __forceinline__ void node_gemm(const float* X1, int ldx1, int K1, con
     if ((njb % 2) == 0 && (njb / 2) * nct >= NW) {   // two output blocks per task share the B split
       const int npair = njb / 2;
       for (int task = wave; task < npair * nct; task += NW)
-        node_task_split<2>(X1, ldx1, K1, X2, ldx2, K2, Ws, winv, bias, act, resid, ldr, Y, ldy, RP, nvalid,
-                           2 * (task % npair), task / npair, lane);
+        node_task_split<2, NT>(X1, ldx1, K1, X2, ldx2, K2, Ws, winv, bias, act, resid, ldr, Y, ldy, RP, nvalid,
+                               2 * (task % npair), task / npair, lane);
     } else {
       for (int task = wave; task < njb * nct; task += NW)
-        node_task_split<1>(X1, ldx1, K1, X2, ldx2, K2, Ws, winv, bias, act, resid, ldr, Y, ldy, RP, nvalid, task % njb,
-                           task / njb, lane);
+        node_task_split<1, NT>(X1, ldx1, K1, X2, ldx2, K2, Ws, winv, bias, act, resid, ldr, Y, ldy, RP, nvalid,
+                               task % njb, task / njb, lane);
     }
     return;
   }
@@ -563,6 +624,19 @@ __device__ __forceinline__ void node_gemm(const float* X1, int ldx1, int K1, con
       node_task<NT, 1>(X1, ldx1, K1, X2, ldx2, K2, W, ldw, bias, act, resid, ldr, Y, ldy, RP, nvalid,
                        task % njb, task / njb, lane);
   }
+}
+
+// in-place split node GEMM (Y aliases X1; the M = 256 tangent kernels' phi_h on macc): output block pairs, at most one
+// task per wave (the host admits these kernels only for RP = 32 rows: (NOUT / 64) tasks <= NW)
+template <int NT, int NW>
+__device__ __forceinline__ void node_gemm_inplace(const float* X1, int ldx1, int K1, const float* X2, int ldx2, int K2,
+                                                  const unsigned* __restrict__ Ws, float winv,
+                                                  const float* __restrict__ bias, int NOUT, bool act, float* Y, int ldy,
+                                                  int RP, int nvalid, int wave, int lane) {
+  const int npair = NOUT >> 6;
+  const bool active = wave < npair;
+  node_task_split<2, NT, true>(X1, ldx1, K1, X2, ldx2, K2, Ws, winv, bias, act, nullptr, 0, Y, ldy, RP, nvalid,
+                               active ? 2 * wave : 0, 0, lane, active);
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -882,6 +956,90 @@ __device__ __forceinline__ void edge_tail(const Net& net, const BlockW& bw, cons
 #endif
 }
 
+// M = 256 tangent kernels: phi_e.0 on the edge itself, [h_s | h_r | |r|^2] W1 + b1 (egnn.py:76-79; no per-node P
+// halves, whose primal + tangent rows would need 132 KB of LDS), as split MFMAs with the node-GEMM fragment layout
+// (host-packed -log2(e) W1, K = 2H + 1 zero-padded to 16-deep k-steps): B = 8 consecutive input features of the
+// lane's edge, gathered from the hb rows (16-B reads), primal and tangent sharing every A fragment.  Output: the
+// log2-domain activation y' = silu_u(u) and its tangent (chain_dual_seq's input form).
+template <int NF>
+__device__ __forceinline__ void edge_layer1_dual(const Net& net, const BlockW& bw, const Lds& s, int rr, int rs,
+                                                 float len2, float dlen2, f32x16 (&X)[NF], f32x16 (&XT)[NF],
+                                                 int lane) {
+  const int kk = lane >> 5, H = net.H, RP = net.RP;
+  const int K = 2 * H + 1, nks = (K + 15) >> 4;
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned*>(launder_uniform(bw.W1_s)),
+                                                                         (short)0, 0x7fffffff, 0x00020000);
+  const int voff = lane * 16;
+  auto feat8 = [&](int ks, bool tan, float (&v)[8]) {
+    const int c0 = 16 * ks + 8 * kk;
+    if (c0 + 8 <= 2 * H) {   // h_s or h_r: 8 consecutive features of one hb row (H is a multiple of 32)
+      const int row = (c0 < H ? rs : rr) + (tan ? RP : 0);
+      const float* src = s.hb + row * s.ld_hb + (c0 < H ? c0 : c0 - H);
+      const f32x4 lo = *reinterpret_cast<const f32x4*>(src);
+      const f32x4 hi = *reinterpret_cast<const f32x4*>(src + 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        v[j] = lo[j];
+        v[4 + j] = hi[j];
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (c0 + j == 2 * H) ? (tan ? dlen2 : len2) : 0.f;
+    }
+  };
+#pragma unroll
+  for (int jb = 0; jb < NF; ++jb) {
+    X[jb] = f32x16{};
+    XT[jb] = f32x16{};
+  }
+  for (int ks = 0; ks < nks; ++ks) {
+    float v[8], vt[8];
+    feat8(ks, false, v);
+    feat8(ks, true, vt);
+    u32x4 B[kPieces], BT[kPieces];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      unsigned pc[kPieces], pt[kPieces];
+      split_pair(v[2 * e], v[2 * e + 1], pc);
+      split_pair(vt[2 * e], vt[2 * e + 1], pt);
+#pragma unroll
+      for (int p = 0; p < kPieces; ++p) {
+        B[p][e] = pc[p];
+        BT[p][e] = pt[p];
+      }
+    }
+    static_for<NF>([&](auto Jc) {
+      constexpr int jb = decltype(Jc)::value;
+      u32x4 A[kPieces];
+#pragma unroll
+      for (int p = 0; p < kPieces; ++p) A[p] = wload(rsrc, voff, ((jb * nks + ks) * kPieces + p) * kPieceBytes);
+      static_for<kTerms>([&](auto Tc) {
+        constexpr int t = decltype(Tc)::value;
+        X[jb] = mfma_split(A[term_w(t)], B[term_x(t)], X[jb]);
+        XT[jb] = mfma_split(A[term_w(t)], BT[term_x(t)], XT[jb]);
+      });
+    });
+  }
+  // u = acc / s - log2(e) b1, the log2-domain SiLU and its tangent
+  constexpr float kNegLn2 = -0.69314718055994531f;
+  const float winv = bw.w1inv;
+#pragma unroll
+  for (int jb = 0; jb < NF; ++jb)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const f32x4 b4 = gptr4(bw.bp_u + net.M + jb * 32 + 8 * q + 4 * kk)[0];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int r = 4 * q + e;
+        const float u = fmaf(X[jb][r], winv, b4[e]);
+        const float du = XT[jb][r] * winv;
+        const float rr = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(u));
+        X[jb][r] = u * rr;
+        XT[jb][r] = rr * fmaf(u * (1.0f - rr), kNegLn2, 1.0f) * du;
+      }
+    }
+}
+
 // one 32-edge tile through phi_e / gate / phi_x  (egnn.py:72-95)
 template <int NF, int NT, int L, int D, int P>
 __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, const Lds& s, int tile, int lane, bool agg) {
@@ -1009,6 +1167,22 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
     STAMP_LANE0(s, kStEdgeTail, t_sub);
     return;
   }
+  if constexpr (Geo<NF, NT, P>::kWideT) {
+    // M = 256 tangent kernels: phi_e.0 per edge, then the sequential dual chains (chain_dual_seq)
+    f32x16 X[NF], XT[NF];
+    edge_layer1_dual<NF>(net, bw, s, rr, rs, len2, dlen2, X, XT, lane);
+    STAMP_LANE0(s, kStEdgeLayer1, t_sub);
+    chain_dual_seq<NF, L - 1>(X, XT, launder_uniform(bw.Ws), s.vecs, lane, true);
+    STAMP_LANE0(s, kStEdgeChainE, t_sub);
+    edge_tail<NF, NT, L, D>(net, bw, s, X, XT, valid, rr, agg_dst, r, dr, length, dlength, lane, agg,
+                            [&](f32x16 (&Y)[NF], f32x16 (&YT)[NF]) {
+                              const unsigned* Wx =
+                                  launder_uniform(bw.Ws + (size_t)(L - 1) * SplitPlan<NF, 1>::GL * kGroupU32);
+                              chain_dual_seq<NF, L>(Y, YT, Wx, s.vecs + (L - 1) * NF * 32, lane, false);
+                            });
+    STAMP_LANE0(s, kStEdgeTail, t_sub);
+    return;
+  }
   // phi_e layer 1 from the per-node halves: pre = P_s[s] + P_r[r] + |r|^2 w_d  (egnn.py:76,79)
   f32x16 X[NF], XT[NF];
   const float* Ps = s.P + rs * s.ld_P;
@@ -1080,6 +1254,7 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
                           float* v_out, float* tan_out) {
   constexpr int kNW = Geo<NF, NT, P>::NW, kNT = Geo<NF, NT, P>::NTHR;
   constexpr bool kSplitG = Geo<NF, NT, P>::kSplit;
+  constexpr bool kSplitN = Geo<NF, NT, P>::kSplitN;   // split node GEMMs (primal split kernels and tangent kernels)
   const int tid = opaque_tid(), lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: task indices stay in SGPRs
   const int N = net.N, H = net.H, T = net.T, M = NF * 32, RP = net.RP, MPW = net.MPW, ND = net.ND;
@@ -1132,7 +1307,7 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
     const bool need_h = k + 1 < net.K;
     // stage this block's chain biases and the w_d / w_g / w_x vectors in LDS (read by every edge tile)
     {
-      const float* be = (kSplitG || Geo<NF, NT, P>::kSplitT) ? bw.be_u : bw.be;
+      const float* be = (kSplitG || Geo<NF, NT, P>::kSplitT || Geo<NF, NT, P>::kWideT) ? bw.be_u : bw.be;
       const float* wd = kSplitG ? bw.wd_u : bw.wd;
       const float* wg = kSplitG ? bw.wg_u : bw.wg;
       const float* wx = kSplitG ? bw.wx_u : bw.wx;
@@ -1147,14 +1322,17 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
       }
     }
     // h <- Dense([h | temb])  (egnn.py:166-167)
-    node_gemm<NT, kNW, kSplitG>(s.hin, s.ld_hin, H + T, nullptr, 0, 0, bw.Wn, bw.Wn_s, bw.ninv, H, bw.bn, H, false, nullptr, 0, s.hb, s.ld_hb, RP,
+    node_gemm<NT, kNW, kSplitN>(s.hin, s.ld_hin, H + T, nullptr, 0, 0, bw.Wn, bw.Wn_s, bw.ninv, H, bw.bn, H, false, nullptr, 0, s.hb, s.ld_hb, RP,
                   nvalid, wave, lane);
     __syncthreads();
     STAMP(s, kStNodeDense);
-    // per-node halves of phi_e layer 1
-    node_gemm<NT, kNW, kSplitG>(s.hb, s.ld_hb, H, nullptr, 0, 0, bw.Wp, bw.Wp_s, bw.pinv, 2 * M, kSplitG ? bw.bp_u : bw.bp, 2 * M, false, nullptr, 0, s.P, s.ld_P, RP,
-                  nvalid, wave, lane);
-    __syncthreads();
+    // per-node halves of phi_e layer 1 (the M = 256 tangent kernels compute layer 1 per edge)
+    if constexpr (!Geo<NF, NT, P>::kWideT) {
+      node_gemm<NT, kNW, kSplitN>(s.hb, s.ld_hb, H, nullptr, 0, 0, bw.Wp, kSplitG ? bw.Wp_s : bw.Wp_sn,
+                                  kSplitG ? bw.pinv : bw.pinv_n, 2 * M, kSplitG ? bw.bp_u : bw.bp, 2 * M, false, nullptr, 0, s.P, s.ld_P, RP,
+                    nvalid, wave, lane);
+      __syncthreads();
+    }
     STAMP(s, kStPGemm);
     // edges
     // tile t runs on wave t mod NW, i.e. SIMD t mod 4: every SIMD gets ceil/floor(ntiles / 4) tiles
@@ -1212,9 +1390,31 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
     }
     STAMP(s, kStNodeUpd);
     // phi_h = MLP((M,)*L + (H,)) on [m_i | h], residual (egnn.py:105-111)
+    if constexpr (Geo<NF, NT, P>::kWideT) {
+      // in place on macc (no P region in these kernels), then macc restarts from +0 for the next block's aggregates
+      node_gemm_inplace<NT, kNW>(s.macc, s.ld_m, M, s.hb, s.ld_hb, H, bw.Wh_sn0, bw.hinv_n0, bw.bh[0], M, true,
+                                 s.macc, s.ld_m, RP, nvalid, wave, lane);
+      __syncthreads();
+      for (int l = 1; l < L; ++l) {
+        node_gemm_inplace<NT, kNW>(s.macc, s.ld_m, M, nullptr, 0, 0, bw.Wh_s[l], bw.hinv[l], bw.bh[l], M, true, s.macc,
+                                   s.ld_m, RP, nvalid, wave, lane);
+        __syncthreads();
+      }
+      node_gemm<NT, kNW, true>(s.macc, s.ld_m, M, nullptr, 0, 0, bw.Wh[L], bw.Wh_s[L], bw.hinv[L], H, bw.bh[L], H, false,
+                               s.hb, s.ld_hb, s.hin, s.ld_hin, RP, nvalid, wave, lane);
+      __syncthreads();
+      for (int idx = tid; idx < R * M; idx += kNT) {
+        const int row = idx / M, c = idx - row * M;
+        s.macc[row * s.ld_m + c] = 0.f;
+      }
+      __syncthreads();
+      STAMP(s, kStPhiH);
+      continue;
+    }
     float* Q0 = s.P;
-    float* Q1 = s.P + (kSplitG ? M + 4 : M + 1);   // 16-B aligned rows for the split node GEMMs
-    node_gemm<NT, kNW, kSplitG>(s.macc, s.ld_m, M, s.hb, s.ld_hb, H, bw.Wh[0], bw.Wh_s[0], bw.hinv[0], M, bw.bh[0], M, true, nullptr, 0, Q0, s.ld_P, RP,
+    float* Q1 = s.P + (kSplitN ? M + 4 : M + 1);   // 16-B aligned rows for the split node GEMMs
+    node_gemm<NT, kNW, kSplitN>(s.macc, s.ld_m, M, s.hb, s.ld_hb, H, bw.Wh[0], kSplitG ? bw.Wh_s[0] : bw.Wh_sn0,
+                                kSplitG ? bw.hinv[0] : bw.hinv_n0, M, bw.bh[0], M, true, nullptr, 0, Q0, s.ld_P, RP,
                   nvalid, wave, lane);
     __syncthreads();
     if (!(kSplitG && net.cross)) {   // atomically accumulated aggregates restart from +0
@@ -1224,12 +1424,12 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
       }
     }
     for (int l = 1; l < L; ++l) {
-      node_gemm<NT, kNW, kSplitG>(Q0, s.ld_P, M, nullptr, 0, 0, bw.Wh[l], bw.Wh_s[l], bw.hinv[l], M, bw.bh[l], M, true, nullptr, 0, Q1, s.ld_P, RP,
+      node_gemm<NT, kNW, kSplitN>(Q0, s.ld_P, M, nullptr, 0, 0, bw.Wh[l], bw.Wh_s[l], bw.hinv[l], M, bw.bh[l], M, true, nullptr, 0, Q1, s.ld_P, RP,
                     nvalid, wave, lane);
       __syncthreads();
       float* tq = Q0; Q0 = Q1; Q1 = tq;
     }
-    node_gemm<NT, kNW, kSplitG>(Q0, s.ld_P, M, nullptr, 0, 0, bw.Wh[L], bw.Wh_s[L], bw.hinv[L], H, bw.bh[L], H, false, s.hb, s.ld_hb, s.hin, s.ld_hin, RP,
+    node_gemm<NT, kNW, kSplitN>(Q0, s.ld_P, M, nullptr, 0, 0, bw.Wh[L], bw.Wh_s[L], bw.hinv[L], H, bw.bh[L], H, false, s.hb, s.ld_hb, s.hin, s.ld_hin, RP,
                   nvalid, wave, lane);
     __syncthreads();
     STAMP(s, kStPhiH);

@@ -147,6 +147,15 @@ class EcnfHandle:
         _lib.check(self.lib.ecnf_molecules_per_workgroup(self._h, int(with_tangent), ctypes.byref(v)))
         return v.value
 
+    def _fp32_available(self, with_tangent: bool) -> bool:
+        """Whether the strict-fp32 kernels exist for this shape (the M = 256 tangent kernels are split-fp16 only)."""
+        prev = self.precision
+        self.set_precision("fp32")
+        try:
+            return self.molecules_per_workgroup(with_tangent) > 0
+        finally:
+            self.set_precision(prev)
+
     def chain_arithmetic(self, with_tangent: bool = False) -> str:
         """Edge-chain arithmetic at the current precision: 'split_f16' (2-piece fp16 split, 3 cross terms),
         'split_bf16' (3-piece bf16 split, 6 cross terms; both chain_split.hpp) or 'fp32_mfma'."""
@@ -207,7 +216,8 @@ class EcnfHandle:
             bad = status != _lib.ECNF_OK
             if bool(bad.any()):
                 st = status.cpu()
-                if fallback and self.precision == "split_f16" and bool((st == _lib.ECNF_E_NONFINITE).any()):
+                if fallback and self.precision == "split_f16" and bool((st == _lib.ECNF_E_NONFINITE).any()) and \
+                        self._fp32_available(divergence != _lib.DIV_NONE):
                     idx = torch.nonzero(status == _lib.ECNF_E_NONFINITE).reshape(-1)
                     self.set_precision("fp32")
                     try:

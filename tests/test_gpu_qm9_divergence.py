@@ -1,0 +1,89 @@
+"""GPU parity of the M = 256 tangent kernels (QM9, Geo::kWideT: per-edge phi_e.0, sequential primal / tangent split
+chains, in-place phi_h) against the CPU oracle: the JVP, the Hutchinson log-density of get_log_prob /
+sample_and_log_prob_cnf on the qm9.yaml network (N = 29), and the exact trace on a small-N M = 256 network.
+
+Reference: setup_training.py:190-203 (get_log_prob on the test set for every config), sample_and_log_prob.py:41-149,
+examples/config/qm9.yaml:5-13.  Tolerances as tests/test_gpu_parity.py: JVP max |err| <= 2e-5 * max(1, |ref|);
+short fixed-step trajectories 1e-4; log-densities 2e-3 absolute."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import ecnf_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+if not torch.cuda.is_available():  # collected on CPU-only hosts, skipped there
+    pytest.skip("needs a ROCm GPU", allow_module_level=True)
+
+from ecnf_amd import CONFIGS, CNFConfig  # noqa: E402
+from ecnf_amd import _lib  # noqa: E402
+from ecnf_amd.engine import SolveOptions  # noqa: E402
+
+from test_gpu_parity import g, rel_err, setup  # noqa: E402
+
+# small-N network of the QM9 widths (M = 256, L = 4) for the exact trace (N * D = 15 tangents per evaluation)
+WIDE_TINY = CNFConfig(n_nodes=5, dim=3, n_features=2, hidden=32, mlp_width=256, mlp_depth=4, n_blocks=2,
+                      base_scale=1.0)
+
+
+def test_qm9_tangent_kernel_exists():
+    cfg = CONFIGS["qm9"]
+    _, _, h, _, _, _ = setup(cfg, B=1)
+    assert h.molecules_per_workgroup(with_tangent=True) == 1
+    assert h.chain_arithmetic(with_tangent=True) == "split_f16"
+
+
+@pytest.mark.parametrize("name", ["qm9"])
+def test_jvp_wide(name):
+    cfg = CONFIGS[name]
+    oc, params, h, z, x0, feat = setup(cfg, B=3)
+    t = np.array([0.1, 0.5, 0.9], np.float32)
+    u = np.random.default_rng(3).standard_normal((3, 2, cfg.event_dim)).astype(np.float32)
+    v, ju = h.jvp(g(x0), g(t), g(feat, torch.int32), g(u))
+    vr, jr = O.egnn_vector_field(params, oc, x0, t, feat, tangents=u, dtype=np.float64)
+    assert rel_err(v, vr) <= 2e-5, rel_err(v, vr)
+    assert rel_err(ju, jr) <= 2e-5, rel_err(ju, jr)
+
+
+def test_qm9_log_prob_hutchinson_fixed():
+    """get_log_prob(approx=True, fixed steps) on qm9.yaml: 1 -> 0, 8 Euler steps."""
+    cfg = CONFIGS["qm9"]
+    oc, params, h, z, x0, feat = setup(cfg, B=2)
+    eps = np.random.default_rng(77).standard_normal(x0.shape).astype(np.float32)
+    x, dl, nfe, st = h.integrate(g(x0), g(feat, torch.int32), 1.0, 0.0, SolveOptions("euler", 0.125),
+                                 divergence=_lib.DIV_HUTCHINSON, eps=g(eps))
+    lp_ref, _, dl_ref, _, x_ref = O.get_log_prob(params, oc, x0, feat, eps=eps, approx=True, solver="euler",
+                                                 dt0=0.125, dtype=np.float64)
+    assert int(nfe.min()) == 8 and int(st.abs().sum()) == 0
+    assert np.abs(x.cpu().numpy() - x_ref).max() <= 1e-4
+    assert np.abs(dl.cpu().numpy() - dl_ref).max() <= 2e-3
+    lp = (h.base_log_prob(x) + dl).cpu().numpy()
+    assert np.abs(lp - lp_ref).max() <= 2e-3
+
+
+def test_qm9_sample_and_log_prob_hutchinson():
+    """sample_and_log_prob_cnf(approx=True, fixed steps) on qm9.yaml: 0 -> 1, Dopri5 dt = 0.25, eps = z."""
+    cfg = CONFIGS["qm9"]
+    oc, params, h, z, x0, feat = setup(cfg, B=2)
+    x1, dl, nfe, _ = h.integrate(g(x0), g(feat, torch.int32), 0.0, 1.0, SolveOptions("dopri5", 0.25),
+                                 divergence=_lib.DIV_HUTCHINSON, eps=g(z))
+    x1r, lq_ref, _ = O.sample_and_log_prob(params, oc, x0, feat, eps=z, approx=True, solver="dopri5", dt0=0.25,
+                                           dtype=np.float64)
+    assert np.abs(x1.cpu().numpy() - x1r).max() <= 1e-4
+    lq = (h.base_log_prob(g(x0)) - dl).cpu().numpy()
+    assert np.abs(lq - lq_ref).max() <= 2e-3
+
+
+def test_wide_log_prob_exact_fixed():
+    """get_log_prob(approx=False): the full N*D trace through the M = 256 tangent kernels (small N)."""
+    cfg = WIDE_TINY
+    oc, params, h, z, x0, feat = setup(cfg, B=3)
+    x, dl, nfe, _ = h.integrate(g(x0), g(feat, torch.int32), 1.0, 0.0, SolveOptions("euler", 0.125),
+                                divergence=_lib.DIV_EXACT)
+    lp_ref, _, dl_ref, _, x_ref = O.get_log_prob(params, oc, x0, feat, approx=False, solver="euler", dt0=0.125,
+                                                 dtype=np.float64)
+    assert np.abs(x.cpu().numpy() - x_ref).max() <= 1e-4
+    assert np.abs(dl.cpu().numpy() - dl_ref).max() <= 2e-3
+    lp = (h.base_log_prob(x) + dl).cpu().numpy()
+    assert np.abs(lp - lp_ref).max() <= 2e-3

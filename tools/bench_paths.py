@@ -33,6 +33,7 @@ CASES = [
     ("aldp", 512, "dopri5", None, "none", "sample"),
     ("aldp", 512, "dopri5", None, "hutchinson", "logp"),
     ("qm9", 2048, "euler", 0.01, "none", "sample"),
+    ("qm9", 512, "euler", 0.01, "hutchinson", "logp"),
 ]
 DIV = {"none": _lib.DIV_NONE, "hutchinson": _lib.DIV_HUTCHINSON, "exact": _lib.DIV_EXACT}
 
@@ -73,8 +74,11 @@ def run_case(name, B, solver, step, div, direction):
 def main():
     out = []
     only = os.environ.get("ECNF_PATHS_ONLY")   # comma-separated config names
+    divs = os.environ.get("ECNF_PATHS_DIV")    # comma-separated divergence kinds
     for case in CASES:
         if only and case[0] not in only.split(","):
+            continue
+        if divs and case[4] not in divs.split(","):
             continue
         t = time.time()
         rec = run_case(*case)
