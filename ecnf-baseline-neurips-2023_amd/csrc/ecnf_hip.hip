@@ -242,8 +242,9 @@ struct ecnf_handle {
   int device;
   float* dbuf;
   int prec;            // ecnf_precision of later calls
-  Net net[4];          // [2 P + NT]
+  Net net[4];          // [2 P + NT], at the LDS-optimal molecules per workgroup (choose_mpw)
   size_t lds[4];       // dynamic LDS bytes per workgroup [2 P + NT]
+  int ncu;             // compute units of the device (batch-aware workgroup sizing, net_for_batch)
 };
 
 namespace {
@@ -369,6 +370,35 @@ bool vec_layout(const ecnf_cfg& c, int NT, int P) {
          wide_tangent(c, NT, P);
 }
 
+// dynamic LDS bytes of one workgroup holding m molecules (RP padded node rows)
+size_t lds_bytes(const ecnf_cfg& c, int NT, int P, int m, int RP) {
+  const int N = c.n_nodes, D = c.dim, H = c.hidden, T = c.time_embedding_dim, M = c.mlp_width;
+  const bool vec = vec_layout(c, NT, P), wide = wide_tangent(c, NT, P);
+  const int floats = (NT ? lds_eval_floats<1>(N, D, H, T, M, m, RP, vec, wide)
+                         : lds_eval_floats<0>(N, D, H, T, M, m, RP, vec)) +
+                     solver_lds_floats(m, N * D);
+  return (size_t)floats * 4;
+}
+
+// the Net fields that depend on the molecules per workgroup: MPW, RP, and the split primal kernels' stored
+// segment parts (cross rows overlaying hin; the receiver segments a tile boundary splits)
+void set_mpw(Net& n, const ecnf_cfg& c, int NT, int P, int mpw, int rp) {
+  const int M = c.mlp_width, H = c.hidden, T = c.time_embedding_dim;
+  n.MPW = mpw;
+  n.RP = rp;
+  const bool vec = split_primal(c, NT, P);
+  n.cross = vec && (size_t)mpw * (n.EP / 32) * ld_node(M, 1, true) <= (size_t)rp * ld_node(H + T, 1, true) &&
+            n.EP / 32 <= kMaxTilesPerMol;
+  n.ncross = 0;
+  const int nn1 = c.n_nodes - 1;
+  for (int t = 1; n.cross && t < n.EP / 32; ++t)
+    if (32 * t < n.E && (32 * t) % nn1 != 0) {
+      n.xs_i[n.ncross] = (unsigned char)((32 * t) / nn1);
+      n.xs_t[n.ncross] = (unsigned char)t;
+      ++n.ncross;
+    }
+}
+
 int choose_mpw(const ecnf_cfg& c, int NT, int P, int* mpw_out, size_t* lds_out, int* rp_out) {
   const int N = c.n_nodes, D = c.dim, H = c.hidden, T = c.time_embedding_dim, M = c.mlp_width;
   const int E = N * (N - 1);
@@ -420,12 +450,63 @@ bool shape_supported(const ecnf_cfg& c, int NT, int P = -1) {
 }
 
 
+// Batch-aware workgroup sizing: the handle's MPW maximises the tile balance of one workgroup, but a batch that
+// fills fewer workgroups than the device has CUs (ALDP B = 512 at MPW = 4: 128 workgroups on 256 CUs) leaves CUs
+// idle.  Pick m <= MPW minimising (workgroup rounds) x (per-workgroup time), with the time of one workgroup taken as
+// its edge tiles per SIMD plus ~0.6 tile-equivalents of node-GEMM work per 32 node rows (LJ13 stamps: node phases ~
+// 18 % beside 5 tiles per SIMD at 2 row tiles); ties keep the larger m.  A molecule's arithmetic does not depend
+// on m (every molecule owns its edge tiles and node rows), so results are bitwise independent of the choice.
+// Adaptive solves: a workgroup runs until its slowest molecule is done, and workgroups of unequal length balance
+// over the CUs as they retire, so the model charges (workgroups / CUs) continuous rounds, plus a per-workgroup
+// penalty per extra molecule for the expected max of m step counts (ECNF_ADAPTIVE_MPW_PENALTY, default 0: measured
+// on ALDP B = 512 PID, penalty 0 / 0.15 / 0.3 -> sample 3.23 / 3.73 / 3.70 ms, Hutchinson log_prob 57.9 / 58.0 /
+// 58.1 ms, profiles/round2/mpw_ab.log).
+double adaptive_penalty() {
+  static const double v = [] {
+    const char* e = std::getenv("ECNF_ADAPTIVE_MPW_PENALTY");
+    return e ? std::atof(e) : 0.0;
+  }();
+  return v;
+}
+
+Net net_for_batch(const ecnf_handle* h, int ix, int B, size_t* lds, bool adaptive = false) {
+  Net n = h->net[ix];
+  *lds = h->lds[ix];
+  const int mpw_max = n.MPW;
+  if (mpw_max <= 1 || B <= 0) return n;
+  const ecnf_cfg& c = h->cfg;
+  const int NT = ix & 1, P = ix >> 1;
+  const int tiles_mol = n.EP / 32;
+  double best = 1e300;
+  int best_m = mpw_max;
+  for (int m = mpw_max; m >= 1; --m) {
+    const int RP = 32 * ((m * c.n_nodes + 31) / 32);
+    const long wgs = (B + m - 1) / m;
+    const double rounds = adaptive ? std::max(1.0, (double)wgs / h->ncu) : (double)((wgs + h->ncu - 1) / h->ncu);
+    const double t_wg = ((double)((m * tiles_mol + kSimds - 1) / kSimds) + 0.6 * (RP / 32)) *
+                        (adaptive ? 1.0 + adaptive_penalty() * (m - 1) : 1.0);
+    const double cost = rounds * t_wg;
+    if (cost < best - 1e-9) {
+      best = cost;
+      best_m = m;
+    }
+  }
+  if (best_m != mpw_max) {
+    const int RP = 32 * ((best_m * c.n_nodes + 31) / 32);
+    set_mpw(n, c, NT, P, best_m, RP);
+    *lds = lds_bytes(c, NT, P, best_m, RP);
+  }
+  return n;
+}
+
 hipError_t dispatch_integrate(const ecnf_handle* h, int NT, const SolveP& sp, const float* y0, const int32_t* feat,
                               const float* eps, float* y1, float* dlogp, int32_t* nfe, int32_t* status, int B,
                               hipStream_t stream) {
   const int M = h->cfg.mlp_width, L = h->cfg.mlp_depth, D = h->cfg.dim, P = h->prec, ix = 2 * P + NT;
+  size_t lds = 0;
+  const Net net = net_for_batch(h, ix, B, &lds, sp.adaptive != 0);
 #define ECNF_CALL(m, l, d, nt, p) \
-  launch_integrate<m / 32, nt, l, d, p>(h->net[ix], h->lds[ix], sp, y0, feat, eps, y1, dlogp, nfe, status, B, stream)
+  launch_integrate<m / 32, nt, l, d, p>(net, lds, sp, y0, feat, eps, y1, dlogp, nfe, status, B, stream)
 #define X(m, l, d)                                                                                           \
   if (M == m && L == l && D == d)                                                                            \
     return NT ? (P ? ECNF_CALL(m, l, d, 1, 1) : ECNF_CALL(m, l, d, 1, 0)) : (P ? ECNF_CALL(m, l, d, 0, 1) : ECNF_CALL(m, l, d, 0, 0));
@@ -443,8 +524,10 @@ hipError_t dispatch_integrate(const ecnf_handle* h, int NT, const SolveP& sp, co
 hipError_t dispatch_vf(const ecnf_handle* h, int NT, const float* x, const float* t, const int32_t* feat,
                        const float* tan_in, int ntan, float* v, float* tan_out, int B, hipStream_t stream) {
   const int M = h->cfg.mlp_width, L = h->cfg.mlp_depth, D = h->cfg.dim, P = h->prec, ix = 2 * P + NT;
+  size_t lds = 0;
+  const Net net = net_for_batch(h, ix, B, &lds);
 #define ECNF_CALL(m, l, d, nt, p) \
-  launch_vf<m / 32, nt, l, d, p>(h->net[ix], h->lds[ix], x, t, feat, tan_in, ntan, v, tan_out, B, stream)
+  launch_vf<m / 32, nt, l, d, p>(net, lds, x, t, feat, tan_in, ntan, v, tan_out, B, stream)
 #define X(m, l, d)                                                                                           \
   if (M == m && L == l && D == d)                                                                            \
     return NT ? (P ? ECNF_CALL(m, l, d, 1, 1) : ECNF_CALL(m, l, d, 1, 0)) : (P ? ECNF_CALL(m, l, d, 0, 1) : ECNF_CALL(m, l, d, 0, 0));
@@ -657,6 +740,10 @@ int ecnf_create(const ecnf_cfg* cfg, const float* params, size_t n_floats, int d
   h->device = device;
   h->dbuf = dbuf;
   h->prec = ECNF_PREC_SPLIT_F16;
+  {
+    hipDeviceProp_t prop;
+    h->ncu = hipGetDeviceProperties(&prop, device) == hipSuccess ? prop.multiProcessorCount : 256;
+  }
   for (int ix = 0; ix < 4; ++ix) {
     const int NT = ix & 1, P = ix >> 1;
     Net& n = h->net[ix];
@@ -701,22 +788,7 @@ int ecnf_create(const ecnf_cfg* cfg, const float* params, size_t n_floats, int d
     int mpw = 0, rp = 0;
     size_t lds = 0;
     if (shape_supported(c, NT, P) && choose_mpw(c, NT, P, &mpw, &lds, &rp) == ECNF_OK) {
-      n.MPW = mpw;
-      n.RP = rp;
-      // split kernels store segment parts; the continuation rows [MPW][EP/32][ld_m] overlay hin (egnn_eval.hpp)
-      const bool vec = split_primal(c, NT, P);
-      n.cross = vec && (size_t)mpw * (n.EP / 32) * ld_node(M, 1, true) <= (size_t)rp * ld_node(H + T, 1, true) &&
-                n.EP / 32 <= kMaxTilesPerMol;
-      // segments (receiver i: edges i(N-1) .. i(N-1)+N-2) that a tile boundary 32t splits; their continuation part
-      // sits in cross row t of the molecule
-      n.ncross = 0;
-      const int nn1 = c.n_nodes - 1;
-      for (int t = 1; n.cross && t < n.EP / 32; ++t)
-        if (32 * t < n.E && (32 * t) % nn1 != 0) {
-          n.xs_i[n.ncross] = (unsigned char)((32 * t) / nn1);
-          n.xs_t[n.ncross] = (unsigned char)t;
-          ++n.ncross;
-        }
+      set_mpw(n, c, NT, P, mpw, rp);
       h->lds[ix] = lds;
     } else {
       n.MPW = 0;
