@@ -617,8 +617,8 @@ int ecnf_create(const ecnf_cfg* cfg, const float* params, size_t n_floats, int d
   Packer pk;
   struct Off {
     size_t Wn, bn, Wp, bp, wd, We, Ws, be, wx, wg, Wh[kMaxPhiH], bh[kMaxPhiH], Wn_s, Wp_s, Wh_s[kMaxPhiH];
-    size_t bp_u, wd_u, be_u, wg_u, wx_u, Wp_sn, Wh_sn0, W1_s;
-    float bx, bg, pinv_n, hinv_n0, w1inv;
+    size_t bp_u, wd_u, be_u, wg_u, wx_u, Wh_sn0, W1_s;
+    float bx, bg, hinv_n0, w1inv;
     float cinv[2 * 4 - 1], ninv, pinv, hinv[kMaxPhiH];
   };
   // packs W [K][NOUT] as split node fragments; returns the offset, *inv = 1 / its scale
@@ -653,7 +653,6 @@ int ecnf_create(const ecnf_cfg* cfg, const float* params, size_t n_floats, int d
     };
     const std::vector<float> wp_u = scaled(wp.data(), wp.size(), kNegLog2e);
     o.Wp_s = put_split_node(wp_u.data(), H, 2 * M, &o.pinv);
-    o.Wp_sn = put_split_node(wp.data(), H, 2 * M, &o.pinv_n);   // natural domain (tangent kernels)
     // the M = 256 tangent kernels' per-edge phi_e.0: [h_s | h_r | |r|^2] rows 0 .. 2H of the kernel, x -log2(e)
     o.W1_s = put_split_node(scaled(b.ek[0], (size_t)(2 * H + 1) * M, kNegLog2e).data(), 2 * H + 1, M, &o.w1inv);
     o.bp_u = pk.put(scaled(bp.data(), bp.size(), kNegLog2e).data(), bp.size());
@@ -778,9 +777,7 @@ int ecnf_create(const ecnf_cfg* cfg, const float* params, size_t n_floats, int d
       w.pinv = o.pinv;
       for (int l = 0; l <= L; ++l) w.hinv[l] = o.hinv[l];
       w.Wp_s = reinterpret_cast<const unsigned*>(dbuf + o.Wp_s);
-      w.Wp_sn = reinterpret_cast<const unsigned*>(dbuf + o.Wp_sn);
       w.Wh_sn0 = reinterpret_cast<const unsigned*>(dbuf + o.Wh_sn0);
-      w.pinv_n = o.pinv_n;
       w.hinv_n0 = o.hinv_n0;
       w.W1_s = reinterpret_cast<const unsigned*>(dbuf + o.W1_s);
       w.w1inv = o.w1inv;

@@ -68,13 +68,16 @@ struct Geo {
   // tangent kernels: the edge chains run split (chain_split_tangent); node GEMMs, layer 1 and the tail stay fp32
   static constexpr bool kSplitT = kSplitTanChain && P == 0 && NT == 1 && NF <= 4;
   // node GEMMs on the split path with 16-B node-row strides: the split primal kernels and (kSplitTanNode) the
-  // M = 128 tangent kernels (the natural-domain fragment copies Wp_sn / Wh_sn0; tangent rows share every A
+  // M = 128 tangent kernels (log2-domain P via the primal Wp_s, natural-domain phi_h.0 copy Wh_sn0; tangent rows share every A
   // fragment).  M = 64 (ALDP) keeps fp32 node GEMMs: the padded 16-B strides would halve its molecules per
   // workgroup (2 -> 1; Hutchinson log_prob 55.9 -> 62.0 ms measured)
   // M = 256 tangent kernels (QM9): per-edge phi_e.0 (no P buffer), sequential primal / tangent split chains
   // (chain_dual_seq), phi_h in place on macc
   static constexpr bool kWideT = kSplitTanChain && P == 0 && NT == 1 && NF == 8;
   static constexpr bool kSplitN = kSplit || (kSplitTanNode && kSplitT && NF == 4) || kWideT;
+  // M = 128 split tangent kernels: P (primal and tangent rows) in the log2 domain (the primal kernels' -log2(e)
+  // fragments), phi_e.0's SiLU and its tangent evaluated there and split straight into the chain's input buffers
+  static constexpr bool kL2T = kSplitT && kSplitN;
 #ifndef ECNF_SPLIT_NW
 #define ECNF_SPLIT_NW 8
 #endif
@@ -125,10 +128,10 @@ struct BlockW {
   // 1 / the power-of-two scale of each split weight matrix (chain_split.hpp): chain layers, Wn, Wp, phi_h
   float cinv[2 * 4 - 1];
   float ninv, pinv, hinv[kMaxPhiH];
-  // natural-domain split fragments for the tangent kernels' P GEMM and phi_h.0 (the primal copies above carry the
-  // log2-domain factors), with their 1 / scale
-  const unsigned* Wp_sn; const unsigned* Wh_sn0;
-  float pinv_n, hinv_n0;
+  // natural-domain split fragments of phi_h.0 for the tangent kernels (the primal copy above carries the message
+  // scale -ln2 / sqrt(N-1)), with its 1 / scale
+  const unsigned* Wh_sn0;
+  float hinv_n0;
   // M = 256 tangent kernels: phi_e.0 kernel [(2H+1)][M] x -log2(e) as split node fragments (edge_layer1_dual)
   const unsigned* W1_s;
   float w1inv;
@@ -1167,6 +1170,67 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
     STAMP_LANE0(s, kStEdgeTail, t_sub);
     return;
   }
+  if constexpr (Geo<NF, NT, P>::kL2T) {
+    // phi_e.0 from the log2-domain per-node halves: u = P_s[s] + P_r[r] + |r|^2 w_d', y' = u / (1 + 2^u) and its
+    // tangent dy' = r du (1 - ln2 (u - y')), split straight into the chain's input buffers (16-B LDS reads)
+    constexpr float kNegLn2 = -0.69314718055994531f;
+    SplitX<NF> XA, XB, XAT, XBT;
+    f32x16 X[NF], XT[NF];
+    const float* Ps = s.P + rs * s.ld_P;
+    const float* Pr = s.P + rr * s.ld_P + M;
+    const float* PsT = s.P + (RP + rs) * s.ld_P;
+    const float* PrT = s.P + (RP + rr) * s.ld_P + M;
+    static_for<NF>([&](auto Fc) {
+      constexpr int fb = decltype(Fc)::value;
+      static_for<4>([&](auto Qc) {
+        constexpr int q = decltype(Qc)::value;
+        const int row = fb * 32 + 8 * q + 4 * kk;
+        const f32x4 w = *reinterpret_cast<const f32x4*>(s.vecs + (2 * L - 1) * (NF * 32) + row);
+        const f32x4 ps = *reinterpret_cast<const f32x4*>(Ps + row);
+        const f32x4 pr = *reinterpret_cast<const f32x4*>(Pr + row);
+        const f32x4 pst = *reinterpret_cast<const f32x4*>(PsT + row);
+        const f32x4 prt = *reinterpret_cast<const f32x4*>(PrT + row);
+        static_for<2>([&](auto Hc) {
+          constexpr int e = 2 * decltype(Hc)::value;
+          float y[2], d[2];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const float u = ps[e + h] + pr[e + h] + len2 * w[e + h];
+            const float du = pst[e + h] + prt[e + h] + dlen2 * w[e + h];
+            const float r = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(u));
+            y[h] = u * r;
+            d[h] = r * du * fmaf(u - y[h], kNegLn2, 1.0f);
+          }
+          put_pair<NF, fb, 4 * q + e>(XA, y[0], y[1]);
+          put_pair<NF, fb, 4 * q + e>(XAT, d[0], d[1]);
+        });
+      });
+    });
+    STAMP_LANE0(s, kStEdgeLayer1, t_sub);
+    ChainInv ie, ix;
+    static_for<2 * 4 - 1>([&](auto Lc) {
+      constexpr int l = decltype(Lc)::value;
+      ie.v[l] = l < L - 1 ? bw.cinv[l] : 1.0f;
+      ix.v[l] = l < L ? bw.cinv[L - 1 + l] : 1.0f;
+    });
+    chain_split<NF, L - 1, 1>(XA, XB, X, launder_uniform(bw.Ws), s.vecs, ie, lane, XAT, XBT, XT);
+#pragma unroll
+    for (int fb = 0; fb < NF; ++fb)
+#pragma unroll
+      for (int r16 = 0; r16 < 16; ++r16) {
+        X[fb][r16] *= kNegLn2;
+        XT[fb][r16] *= kNegLn2;
+      }
+    STAMP_LANE0(s, kStEdgeChainE, t_sub);
+    edge_tail<NF, NT, L, D>(net, bw, s, X, XT, valid, rr, agg_dst, r, dr, length, dlength, lane, agg,
+                            [&](f32x16 (&Y)[NF], f32x16 (&YT)[NF]) {
+                              const unsigned* Wx =
+                                  launder_uniform(bw.Ws + (size_t)(L - 1) * SplitPlan<NF, 1>::GL * kGroupU32);
+                              chain_split_tangent<NF, L>(Y, YT, Wx, s.vecs + (L - 1) * NF * 32, ix, lane);
+                            });
+    STAMP_LANE0(s, kStEdgeTail, t_sub);
+    return;
+  }
   if constexpr (Geo<NF, NT, P>::kWideT) {
     // M = 256 tangent kernels: phi_e.0 per edge, then the sequential dual chains (chain_dual_seq)
     f32x16 X[NF], XT[NF];
@@ -1308,7 +1372,7 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
     // stage this block's chain biases and the w_d / w_g / w_x vectors in LDS (read by every edge tile)
     {
       const float* be = (kSplitG || Geo<NF, NT, P>::kSplitT || Geo<NF, NT, P>::kWideT) ? bw.be_u : bw.be;
-      const float* wd = kSplitG ? bw.wd_u : bw.wd;
+      const float* wd = (kSplitG || Geo<NF, NT, P>::kL2T) ? bw.wd_u : bw.wd;
       const float* wg = kSplitG ? bw.wg_u : bw.wg;
       const float* wx = kSplitG ? bw.wx_u : bw.wx;
       for (int idx = tid; idx < (2 * L + 2) * M; idx += kNT) {
@@ -1328,9 +1392,9 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
     STAMP(s, kStNodeDense);
     // per-node halves of phi_e layer 1 (the M = 256 tangent kernels compute layer 1 per edge)
     if constexpr (!Geo<NF, NT, P>::kWideT) {
-      node_gemm<NT, kNW, kSplitN>(s.hb, s.ld_hb, H, nullptr, 0, 0, bw.Wp, kSplitG ? bw.Wp_s : bw.Wp_sn,
-                                  kSplitG ? bw.pinv : bw.pinv_n, 2 * M, kSplitG ? bw.bp_u : bw.bp, 2 * M, false, nullptr, 0, s.P, s.ld_P, RP,
-                    nvalid, wave, lane);
+      constexpr bool kPu = kSplitG || Geo<NF, NT, P>::kL2T;   // log2-domain P
+      node_gemm<NT, kNW, kSplitN>(s.hb, s.ld_hb, H, nullptr, 0, 0, bw.Wp, bw.Wp_s, bw.pinv, 2 * M,
+                                  kPu ? bw.bp_u : bw.bp, 2 * M, false, nullptr, 0, s.P, s.ld_P, RP, nvalid, wave, lane);
       __syncthreads();
     }
     STAMP(s, kStPGemm);
