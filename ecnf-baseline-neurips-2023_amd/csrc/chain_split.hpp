@@ -624,8 +624,9 @@ __device__ __forceinline__ void chain_dual_seq(f32x16 (&X)[NF], f32x16 (&XT)[NF]
       for (int r = 0; r < 16; ++r) {
         const float u = X[fb][r];
         const float rr = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(u));
-        X[fb][r] = u * rr;
-        XT[fb][r] = rr * fmaf(u * (1.0f - rr), kNegLn2, 1.0f) * XT[fb][r];
+        const float y = u * rr;
+        X[fb][r] = y;
+        XT[fb][r] = rr * XT[fb][r] * fmaf(u - y, kNegLn2, 1.0f);
       }
     __builtin_amdgcn_sched_barrier(0);
   }

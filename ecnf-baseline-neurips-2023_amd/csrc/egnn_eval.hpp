@@ -1037,8 +1037,9 @@ __device__ __forceinline__ void edge_layer1_dual(const Net& net, const BlockW& b
         const float u = fmaf(X[jb][r], winv, b4[e]);
         const float du = XT[jb][r] * winv;
         const float rr = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(u));
-        X[jb][r] = u * rr;
-        XT[jb][r] = rr * fmaf(u * (1.0f - rr), kNegLn2, 1.0f) * du;
+        const float y = u * rr;
+        X[jb][r] = y;
+        XT[jb][r] = rr * du * fmaf(u - y, kNegLn2, 1.0f);
       }
     }
 }
@@ -1214,19 +1215,22 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
       ix.v[l] = l < L ? bw.cinv[L - 1 + l] : 1.0f;
     });
     chain_split<NF, L - 1, 1>(XA, XB, X, launder_uniform(bw.Ws), s.vecs, ie, lane, XAT, XBT, XT);
-#pragma unroll
-    for (int fb = 0; fb < NF; ++fb)
-#pragma unroll
-      for (int r16 = 0; r16 < 16; ++r16) {
-        X[fb][r16] *= kNegLn2;
-        XT[fb][r16] *= kNegLn2;
-      }
     STAMP_LANE0(s, kStEdgeChainE, t_sub);
+    // the tail stays in the log2 domain as in the primal split kernels: gate / shift with the -ln2-folded w_g', w_x'
+    // (staged in vecs), the aggregate's -ln2 / sqrt(N-1) in the split phi_h.0 weights, phi_x fed the messages as is
     edge_tail<NF, NT, L, D>(net, bw, s, X, XT, valid, rr, agg_dst, r, dr, length, dlength, lane, agg,
                             [&](f32x16 (&Y)[NF], f32x16 (&YT)[NF]) {
                               const unsigned* Wx =
                                   launder_uniform(bw.Ws + (size_t)(L - 1) * SplitPlan<NF, 1>::GL * kGroupU32);
-                              chain_split_tangent<NF, L>(Y, YT, Wx, s.vecs + (L - 1) * NF * 32, ix, lane);
+                              static_for<NF>([&](auto Fc) {
+                                constexpr int fb = decltype(Fc)::value;
+                                static_for<8>([&](auto Ic) {
+                                  constexpr int i = decltype(Ic)::value;
+                                  put_pair<NF, fb, 2 * i>(XA, Y[fb][2 * i], Y[fb][2 * i + 1]);
+                                  put_pair<NF, fb, 2 * i>(XAT, YT[fb][2 * i], YT[fb][2 * i + 1]);
+                                });
+                              });
+                              chain_split<NF, L, 1>(XA, XB, Y, Wx, s.vecs + (L - 1) * NF * 32, ix, lane, XAT, XBT, YT);
                             });
     STAMP_LANE0(s, kStEdgeTail, t_sub);
     return;
@@ -1373,8 +1377,8 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
     {
       const float* be = (kSplitG || Geo<NF, NT, P>::kSplitT || Geo<NF, NT, P>::kWideT) ? bw.be_u : bw.be;
       const float* wd = (kSplitG || Geo<NF, NT, P>::kL2T) ? bw.wd_u : bw.wd;
-      const float* wg = kSplitG ? bw.wg_u : bw.wg;
-      const float* wx = kSplitG ? bw.wx_u : bw.wx;
+      const float* wg = (kSplitG || Geo<NF, NT, P>::kL2T) ? bw.wg_u : bw.wg;
+      const float* wx = (kSplitG || Geo<NF, NT, P>::kL2T) ? bw.wx_u : bw.wx;
       for (int idx = tid; idx < (2 * L + 2) * M; idx += kNT) {
         const int v = idx / M, c = idx - v * M;
         float val;
@@ -1437,7 +1441,7 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
           for (int c = lane; c < M; c += 64) dst[c] += src[c];
         }
       }
-    } else {
+    } else if constexpr (!Geo<NF, NT, P>::kL2T) {   // kL2T: the scale is in the split phi_h.0 weights
       for (int idx = tid; idx < R * M; idx += kNT) {
         const int row = idx / M, c = idx - row * M;
         s.macc[row * s.ld_m + c] = s.macc[row * s.ld_m + c] / net.sqrt_nn1;
@@ -1477,8 +1481,9 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
     }
     float* Q0 = s.P;
     float* Q1 = s.P + (kSplitN ? M + 4 : M + 1);   // 16-B aligned rows for the split node GEMMs
-    node_gemm<NT, kNW, kSplitN>(s.macc, s.ld_m, M, s.hb, s.ld_hb, H, bw.Wh[0], kSplitG ? bw.Wh_s[0] : bw.Wh_sn0,
-                                kSplitG ? bw.hinv[0] : bw.hinv_n0, M, bw.bh[0], M, true, nullptr, 0, Q0, s.ld_P, RP,
+    constexpr bool kHu = kSplitG || Geo<NF, NT, P>::kL2T;   // log2-domain messages, scale in phi_h.0
+    node_gemm<NT, kNW, kSplitN>(s.macc, s.ld_m, M, s.hb, s.ld_hb, H, bw.Wh[0], kHu ? bw.Wh_s[0] : bw.Wh_sn0,
+                                kHu ? bw.hinv[0] : bw.hinv_n0, M, bw.bh[0], M, true, nullptr, 0, Q0, s.ld_P, RP,
                   nvalid, wave, lane);
     __syncthreads();
     if (!(kSplitG && net.cross)) {   // atomically accumulated aggregates restart from +0
