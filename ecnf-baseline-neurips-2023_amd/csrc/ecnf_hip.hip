@@ -366,7 +366,7 @@ bool wide_tangent(const ecnf_cfg& c, int NT, int P) { return NT && P == 0 && c.m
 // Geo<NF, NT, P>::kSplitN: split node GEMMs, i.e. 16-B node-row strides (split primal kernels and, with
 // kSplitTanNode, the split tangent kernels)
 bool vec_layout(const ecnf_cfg& c, int NT, int P) {
-  return split_primal(c, NT, P) || (kSplitTanNode && kSplitTanChain && P == 0 && NT && c.mlp_width == 128) ||
+  return split_primal(c, NT, P) || (kSplitTanNode && kSplitTanChain && P == 0 && NT && c.mlp_width <= 128) ||
          wide_tangent(c, NT, P);
 }
 
@@ -374,8 +374,8 @@ bool vec_layout(const ecnf_cfg& c, int NT, int P) {
 size_t lds_bytes(const ecnf_cfg& c, int NT, int P, int m, int RP) {
   const int N = c.n_nodes, D = c.dim, H = c.hidden, T = c.time_embedding_dim, M = c.mlp_width;
   const bool vec = vec_layout(c, NT, P), wide = wide_tangent(c, NT, P);
-  const int floats = (NT ? lds_eval_floats<1>(N, D, H, T, M, m, RP, vec, wide)
-                         : lds_eval_floats<0>(N, D, H, T, M, m, RP, vec)) +
+  const int floats = (NT ? lds_eval_floats<1>(N, D, H, T, M, c.mlp_depth, m, RP, vec, wide)
+                         : lds_eval_floats<0>(N, D, H, T, M, c.mlp_depth, m, RP, vec)) +
                      solver_lds_floats(m, N * D);
   return (size_t)floats * 4;
 }
@@ -412,8 +412,8 @@ int choose_mpw(const ecnf_cfg& c, int NT, int P, int* mpw_out, size_t* lds_out, 
     const int RP = 32 * ((m * N + 31) / 32);
     const bool vec = vec_layout(c, NT, P), wide = wide_tangent(c, NT, P);
     if (wide && RP != 32) break;   // in-place phi_h: one 32-row node tile (node_gemm_inplace)
-    const int floats = (NT ? lds_eval_floats<1>(N, D, H, T, M, m, RP, vec, wide)
-                           : lds_eval_floats<0>(N, D, H, T, M, m, RP, vec)) +
+    const int floats = (NT ? lds_eval_floats<1>(N, D, H, T, M, c.mlp_depth, m, RP, vec, wide)
+                           : lds_eval_floats<0>(N, D, H, T, M, c.mlp_depth, m, RP, vec)) +
                        solver_lds_floats(m, N * D);
     const size_t bytes = (size_t)floats * 4;
     if (bytes > 160 * 1024) break;

@@ -68,14 +68,14 @@ struct Geo {
   // tangent kernels: the edge chains run split (chain_split_tangent); node GEMMs, layer 1 and the tail stay fp32
   static constexpr bool kSplitT = kSplitTanChain && P == 0 && NT == 1 && NF <= 4;
   // node GEMMs on the split path with 16-B node-row strides: the split primal kernels and (kSplitTanNode) the
-  // M = 128 tangent kernels (log2-domain P via the primal Wp_s, natural-domain phi_h.0 copy Wh_sn0; tangent rows share every A
-  // fragment).  M = 64 (ALDP) keeps fp32 node GEMMs: the padded 16-B strides would halve its molecules per
-  // workgroup (2 -> 1; Hutchinson log_prob 55.9 -> 62.0 ms measured)
+  // M <= 128 tangent kernels (log2-domain P via the primal Wp_s; tangent rows share every A fragment).  (The padded
+  // 16-B strides fit ALDP's M = 64 tangent kernel at 2 molecules per workgroup only since the x_c0 copy left LDS
+  // and vecs is sized by L: before, split node GEMMs dropped it to 1, 55.9 -> 62.0 ms.)
   // M = 256 tangent kernels (QM9): per-edge phi_e.0 (no P buffer), sequential primal / tangent split chains
   // (chain_dual_seq), phi_h in place on macc
   static constexpr bool kWideT = kSplitTanChain && P == 0 && NT == 1 && NF == 8;
-  static constexpr bool kSplitN = kSplit || (kSplitTanNode && kSplitT && NF == 4) || kWideT;
-  // M = 128 split tangent kernels: P (primal and tangent rows) in the log2 domain (the primal kernels' -log2(e)
+  static constexpr bool kSplitN = kSplit || (kSplitTanNode && kSplitT) || kWideT;
+  // M <= 128 split tangent kernels: P (primal and tangent rows) in the log2 domain (the primal kernels' -log2(e)
   // fragments), phi_e.0's SiLU and its tangent evaluated there and split straight into the chain's input buffers
   static constexpr bool kL2T = kSplitT && kSplitN;
 #ifndef ECNF_SPLIT_NW
@@ -200,7 +200,6 @@ struct Lds {
   float* P;    int ld_P;     // [R][2M]   per-node phi_e.0 halves; reused as phi_h ping-pong
   float* macc; int ld_m;     // [R][M]    message aggregate
   float* xc;                 // [R][D]    centred positions, updated per block
-  float* xc0;                // [R][D]    initial centred positions
   float* dxacc;              // [R][D]    shift aggregate
   float* mean;               // [2][MPW][D] input mean (primal, tangent)
   float* temb;               // [MPW][T]
@@ -225,7 +224,7 @@ __host__ __device__ inline int ld_node(int k, int odd_pad, bool vec) {
 }
 
 template <int NT>
-__host__ __device__ inline int lds_eval_floats(int N, int D, int H, int T, int M, int MPW, int RP, bool vec,
+__host__ __device__ inline int lds_eval_floats(int N, int D, int H, int T, int M, int L, int MPW, int RP, bool vec,
                                                bool noP = false) {
   const int R = RP * (1 + NT);
   int n = 0;
@@ -233,10 +232,10 @@ __host__ __device__ inline int lds_eval_floats(int N, int D, int H, int T, int M
   n += align4(R * ld_node(H, 1, vec));
   if (!noP) n += align4(R * ld_node(2 * M, 3, vec));
   n += align4(R * ld_node(M, 1, vec));
-  n += 3 * align4(R * D);
+  n += 2 * align4(R * D);
   n += align4(2 * MPW * D);
   n += align4(MPW * T);
-  n += align4((2 * 4 + 2) * M);   // vecs, sized for L <= 4
+  n += align4((2 * L + 2) * M);   // vecs: 2L - 1 chain biases, w_d, w_g, w_x
   n += align4(MPW * N);
 #ifdef ECNF_STAMPS
   n += 64;   // 32 x u64 stamp slots
@@ -256,11 +255,10 @@ __device__ inline Lds carve_lds(const Net& net, float* base) {
   if (!NOP) p += align4(R * s.ld_P);
   s.macc = p; s.ld_m = ld_node(net.M, 1, VEC);           p += align4(R * s.ld_m);
   s.xc = p;    p += align4(R * net.D);
-  s.xc0 = p;   p += align4(R * net.D);
   s.dxacc = p; p += align4(R * net.D);
   s.mean = p;  p += align4(2 * net.MPW * net.D);
   s.temb = p;  p += align4(net.MPW * net.T);
-  s.vecs = p;  p += align4((2 * 4 + 2) * net.M);
+  s.vecs = p;  p += align4((2 * net.L + 2) * net.M);
   s.feat = reinterpret_cast<int*>(p); p += align4(net.MPW * net.N);
 #ifdef ECNF_STAMPS
   s.stamps = reinterpret_cast<unsigned long long*>(p); p += 64;
@@ -1351,7 +1349,6 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
     const float v = src[m * ND + (n - m * N) * D + d] - s.mean[which * MPW * D + m * D + d];
     const int row = which * RP + n;
     s.xc[row * D + d] = v;
-    s.xc0[row * D + d] = v;
   }
   for (int idx = tid; idx < R * (H + T); idx += kNT) {
     const int row = idx / (H + T), c = idx - row * (H + T);
@@ -1509,7 +1506,11 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
     const int which = idx / (nvalid * D), nd = idx - which * nvalid * D, n = nd / D, d = nd - n * D;
     const int m = n / N;
     const int row = which * RP + n;
-    const float v = ((s.xc[row * D + d] - s.xc0[row * D + d]) - s.mean[which * MPW * D + m * D + d]) * net.fs;
+    // x_c0 recomputed from the (unchanged) input exactly as the prologue computed it (no [R][D] LDS copy)
+    const float* src = which == 0 ? x_in : tan_in;
+    const float mu = s.mean[which * MPW * D + m * D + d];
+    const float xc0 = src[m * ND + (n - m * N) * D + d] - mu;
+    const float v = ((s.xc[row * D + d] - xc0) - mu) * net.fs;
     float* dst = which == 0 ? v_out : tan_out;
     dst[m * ND + (n - m * N) * D + d] = v;
   }
