@@ -495,6 +495,7 @@ Net net_for_batch(const ecnf_handle* h, int ix, int B, size_t* lds, bool adaptiv
     const int RP = 32 * ((best_m * c.n_nodes + 31) / 32);
     set_mpw(n, c, NT, P, best_m, RP);
     *lds = lds_bytes(c, NT, P, best_m, RP);
+    n.lds_floats = (int)(*lds / 4);
   }
   return n;
 }
@@ -550,6 +551,24 @@ hipError_t dispatch_vf(const ecnf_handle* h, int NT, const float* x, const float
 extern "C" {
 
 int ecnf_abi_version(void) { return ECNF_ABI_VERSION; }
+
+#ifdef ECNF_DEVICE_CHECKS
+// device-checked diagnostic build only: OR of the failed-check bits of every kernel since the last reset
+int ecnf_debug_checks(uint32_t* flags, int reset) {
+  if (!flags) return fail(ECNF_E_INVALID, "NULL argument");
+  HIP_TRY(hipDeviceSynchronize());
+  unsigned w[64];
+  HIP_TRY(hipMemcpyFromSymbol(w, HIP_SYMBOL(g_checks), sizeof(w)));
+  unsigned acc = 0;
+  for (unsigned v : w) acc |= v;
+  *flags = acc;
+  if (reset) {
+    unsigned z[64] = {0};
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_checks), z, sizeof(z)));
+  }
+  return ECNF_OK;
+}
+#endif
 
 #ifdef ECNF_STAMPS
 // diagnostic build only: copy (and optionally reset) the accumulated phase cycles
@@ -786,6 +805,7 @@ int ecnf_create(const ecnf_cfg* cfg, const float* params, size_t n_floats, int d
     size_t lds = 0;
     if (shape_supported(c, NT, P) && choose_mpw(c, NT, P, &mpw, &lds, &rp) == ECNF_OK) {
       set_mpw(n, c, NT, P, mpw, rp);
+      n.lds_floats = (int)(lds / 4);
       h->lds[ix] = lds;
     } else {
       n.MPW = 0;

@@ -146,6 +146,8 @@ __global__ __launch_bounds__((Geo<NF, NT, P>::NTHR)) void integrate_kernel(Net n
   const int mol0 = blockIdx.x * MPW;
   const int nmol = min(MPW, B - mol0);
   const int a = align4(MPW * ND), b = align4(MPW);
+  ECNF_DCHECK((int)(s.tail - smem) + solver_lds_floats(MPW, ND) <= net.lds_floats, 0);
+  ECNF_DCHECK(nmol >= 1 && nmol <= MPW, 5);
   const bool track = sp.div != ECNF_DIV_NONE;
 
   // zero the eval scratch (aggregates must start at +0; padding rows stay finite)
@@ -395,6 +397,8 @@ __global__ __launch_bounds__((Geo<NF, NT, P>::NTHR)) void vf_kernel(Net net, con
   const SolverLds st = carve_solver(s.tail, MPW, ND);
   const int mol0 = blockIdx.x * MPW;
   const int nmol = min(MPW, B - mol0);
+  ECNF_DCHECK((int)(s.tail - smem) + solver_lds_floats(MPW, ND) <= net.lds_floats, 0);
+  ECNF_DCHECK(nmol >= 1 && nmol <= MPW, 5);
   for (int i = tid; i < (int)(s.tail - smem); i += kThreads) smem[i] = 0.f;
   __syncthreads();
   for (int i = tid; i < MPW * ND; i += kThreads) st.ys[i] = (i / ND) < nmol ? x[(size_t)mol0 * ND + i] : 0.f;

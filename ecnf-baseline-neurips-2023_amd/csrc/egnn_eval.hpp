@@ -142,6 +142,7 @@ struct Net {
   int E;          // N (N - 1)
   int EP;         // edges per molecule padded to a multiple of 32 (every molecule starts on a tile boundary)
   int MPW;        // molecules per workgroup
+  int lds_floats; // dynamic LDS of one workgroup (device-checked build: ECNF_DCHECK bit 0)
   int RP;         // padded primal node rows
   int ND;         // N * D
   float C;        // EGCL normalization constant
@@ -189,6 +190,25 @@ __device__ unsigned long long g_stamps[32];
 #define ECNF_STAMP_DECL
 #define STAMP(s, slot) do {} while (0)
 #define STAMP_LANE0(s, slot, t0) do {} while (0)
+#endif
+
+// ---------------------------------------------------------------------------------------------------
+// device-side bounds checks (separate diagnostic build, -DECNF_DEVICE_CHECKS): a failed check
+// ORs its bit into g_checks (one word per lane, vector atomics) and the kernel carries on; ecnf_debug_checks() reads
+// and clears the words.  Never compiled into the product library.
+//   bit 0  LDS carve-up + solver state past the launch's dynamic LDS      bit 1  edge receiver / sender row out of range
+//   bit 2  edge tile past the workgroup's tiles                           bit 3  node-GEMM row tile past RP
+//   bit 4  stored segment part (cross row) out of range                    bit 5  molecule slot past the workgroup
+// ---------------------------------------------------------------------------------------------------
+#ifdef ECNF_DEVICE_CHECKS
+__device__ unsigned g_checks[64];
+#define ECNF_DCHECK(cond, bit)                                                                           \
+  do {                                                                                                   \
+    if (!(cond)) __hip_atomic_fetch_or(&g_checks[threadIdx.x & 63], 1u << (bit), __ATOMIC_RELAXED,       \
+                                       __HIP_MEMORY_SCOPE_AGENT);                                        \
+  } while (0)
+#else
+#define ECNF_DCHECK(cond, bit) do {} while (0)
 #endif
 
 // ---------------------------------------------------------------------------------------------------
@@ -463,6 +483,7 @@ __device__ __forceinline__ void node_task_split(const float* X1, int ldx1, int K
   ct = __builtin_amdgcn_readfirstlane(ct);
   const int kk = lane >> 5, li = lane & 31;
   const int n = ct * 32 + li;
+  ECNF_DCHECK(!active || ct * 32 < RP, 3);
   const int nks1 = (K1 + 15) >> 4, nks = nks1 + ((K2 + 15) >> 4);
   // biases are added in the epilogue: their load latency hides behind the k-loop
   f32x4 bq[NA][4];
@@ -1078,6 +1099,8 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
   if (sd >= N) sd -= N;
   const int mrow = valid ? mol : 0;
   const int rr = mrow * N + i, rs = mrow * N + sd;   // receiver / sender rows (graph.py:10-13)
+  ECNF_DCHECK(rr < net.MPW * N && rs < net.MPW * N && rr >= 0 && rs >= 0, 1);
+  ECNF_DCHECK(tile * 32 < net.MPW * net.EP, 2);
   // split kernels: the row this lane's receiver-segment part is stored to — macc for the part in the tile where
   // the segment starts, the cross buffer (one row per molecule tile) for its continuation in the next tile
   float* agg_dst = nullptr;
@@ -1085,6 +1108,7 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
     if (net.cross) {
       const int tloc = tile - mrow * (net.EP >> 5);
       agg_dst = tloc == ((i * nn1) >> 5) ? s.macc + rr * s.ld_m : s.cross + (mrow * (net.EP >> 5) + tloc) * s.ld_m;
+      ECNF_DCHECK(tloc >= 0 && mrow * (net.EP >> 5) + tloc < net.MPW * (net.EP >> 5), 4);
     }
   }
 #ifdef ECNF_STAMPS
