@@ -256,7 +256,7 @@ __device__ __forceinline__ void chain_split(SplitX<NF>& XA, SplitX<NF>& XB, f32x
 #pragma unroll
     for (int p = 0; p < kPieces; ++p) wbuf[gg][p] = wload(rsrc, voff, (gg * kPieces + p) * kPieceBytes);
   // per-item pipeline registers (SSA after unrolling: only live items occupy registers)
-  f32x2 bv[NI], uv[NI], ev[NI], dv[NI];
+  f32x2 bv[NI], uv[NI], ev[NI], dv[NI], e2v[NI];
 #ifdef ECNF_CHAIN_BIAS_INIT
   // each output block's accumulator starts at its (log2-domain) bias column and the weights are unscaled, so stage
   // A needs no FMA; a block's 16 biases (rows acc_row(r, kk)) are 4 x 16-B LDS reads, issued 2 groups ahead
@@ -322,10 +322,11 @@ __device__ __forceinline__ void chain_split(SplitX<NF>& XA, SplitX<NF>& XB, f32x
         const f32x16 z = {};
 #ifdef ECNF_CHAIN_BIAS_INIT
         acc[jb] = mfma_split(A[pa], B[pb], cb);
+        if constexpr (NT) accT[jb] = mfma_split(A[pa], BT[pb], NT == 2 ? cb : z);
 #else
         acc[jb] = mfma_split(A[pa], B[pb], z);
-#endif
         if constexpr (NT) accT[jb] = mfma_split(A[pa], BT[pb], z);
+#endif
       } else {
         acc[jb] = mfma_split(A[pa], B[pb], acc[jb]);
         if constexpr (NT) accT[jb] = mfma_split(A[pa], BT[pb], accT[jb]);
@@ -366,7 +367,12 @@ __device__ __forceinline__ void chain_split(SplitX<NF>& XA, SplitX<NF>& XB, f32x
       ev[id][0] = __builtin_amdgcn_exp2f(uv[id][0]);
       ev[id][1] = __builtin_amdgcn_exp2f(uv[id][1]);
 #endif
-      if constexpr (NT) {
+      if constexpr (NT == 2) {   // a second, independent tile on the same weight fragments
+        dv[id][0] = accT[it.j][r];
+        dv[id][1] = accT[it.j][r + 1];
+        e2v[id][0] = __builtin_amdgcn_exp2f(dv[id][0]);
+        e2v[id][1] = __builtin_amdgcn_exp2f(dv[id][1]);
+      } else if constexpr (NT) {
 #ifdef ECNF_CHAIN_BIAS_INIT
         dv[id][0] = accT[it.j][r];
         dv[id][1] = accT[it.j][r + 1];
@@ -387,6 +393,10 @@ __device__ __forceinline__ void chain_split(SplitX<NF>& XA, SplitX<NF>& XB, f32x
       ev[id][0] = __builtin_amdgcn_rcpf(1.0f + ev[id][0]);
       ev[id][1] = __builtin_amdgcn_rcpf(1.0f + ev[id][1]);
 #endif
+      if constexpr (NT == 2) {
+        e2v[id][0] = __builtin_amdgcn_rcpf(1.0f + e2v[id][0]);
+        e2v[id][1] = __builtin_amdgcn_rcpf(1.0f + e2v[id][1]);
+      }
     }); };
     // stage C
     auto stageC = [&](auto Late) { static_for<Plan::count_l(gg, 2, decltype(Late)::value)>([&](auto Kc) {
@@ -404,7 +414,16 @@ __device__ __forceinline__ void chain_split(SplitX<NF>& XA, SplitX<NF>& XB, f32x
         acc[it.j][2 * it.p] = y0;
         acc[it.j][2 * it.p + 1] = y1;
       }
-      if constexpr (NT) {
+      if constexpr (NT == 2) {
+        const float z0 = dv[id][0] * e2v[id][0];
+        const float z1 = dv[id][1] * e2v[id][1];
+        if constexpr (it.l < NL - 1) {
+          put_pair<NF, it.j, 2 * it.p>(pick<(it.l + 1) & 1>(XAT, XBT), z0, z1);
+        } else {
+          accT[it.j][2 * it.p] = z0;
+          accT[it.j][2 * it.p + 1] = z1;
+        }
+      } else if constexpr (NT) {
         constexpr float kNegLn2 = -0.69314718055994531f;
         // u (1 - r) = u - y' (y' = u r): 4 VALU per element instead of 5
         const float d0 = ev[id][0] * dv[id][0] * fmaf(uv[id][0] - y0, kNegLn2, 1.0f);

@@ -29,6 +29,35 @@ __global__ __launch_bounds__(64 * WAVES) void kern(const unsigned* __restrict__ 
   ChainInv inv;
   for (int l = 0; l < 7; ++l) inv.v[l] = 1.0f / 4096;
   unsigned long long t0 = __builtin_amdgcn_s_memtime();
+#ifdef TWO_TILES   // two tiles per wave share every weight fragment (chain_split NT = 2): TILES / 2 pairs
+  SplitX<NF> XA2, XB2;
+  f32x16 acc2[NF];
+  for (int f = 0; f < NF; ++f)
+    for (int u = 0; u < 2; ++u)
+      for (int p = 0; p < kPieces; ++p) XA2.v[f][u][p] = u32x4{0x3f803f81u + lane, 0x3f01u + f, 0x3e803e81u + u, 0x3c013c00u + p};
+  for (int t = 0; t < TILES / 2; ++t) {
+    chain_split<NF, 2, 2>(XA, XB, acc, launder_uniform(W), bias, inv, lane, XA2, XB2, acc2);
+    static_for<NF>([&](auto Fc) {
+      constexpr int fb = decltype(Fc)::value;
+      static_for<8>([&](auto Ic) {
+        constexpr int i = decltype(Ic)::value;
+        put_pair<NF, fb, 2 * i>(XA, acc[fb][2 * i], acc[fb][2 * i + 1]);
+        put_pair<NF, fb, 2 * i>(XA2, acc2[fb][2 * i], acc2[fb][2 * i + 1]);
+      });
+    });
+    chain_split<NF, 3, 2>(XA, XB, acc, launder_uniform(W + 2 * kLayerU32), bias + 2 * M, inv, lane, XA2, XB2, acc2);
+    static_for<NF>([&](auto Fc) {
+      constexpr int fb = decltype(Fc)::value;
+      static_for<8>([&](auto Ic) {
+        constexpr int i = decltype(Ic)::value;
+        put_pair<NF, fb, 2 * i>(XA, acc[fb][2 * i], acc[fb][2 * i + 1]);
+        put_pair<NF, fb, 2 * i>(XA2, acc2[fb][2 * i], acc2[fb][2 * i + 1]);
+      });
+    });
+  }
+  for (int f = 0; f < NF; ++f)
+    for (int r = 0; r < 16; ++r) acc[f][r] += acc2[f][r];
+#else
   for (int t = 0; t < TILES; ++t) {
     chain_split<NF, 2>(XA, XB, acc, launder_uniform(W), bias, inv, lane);
     static_for<NF>([&](auto Fc) {
@@ -47,6 +76,7 @@ __global__ __launch_bounds__(64 * WAVES) void kern(const unsigned* __restrict__ 
       });
     });
   }
+#endif
   unsigned long long t1 = __builtin_amdgcn_s_memtime();
   float s = 0.f;
   for (int f = 0; f < NF; ++f)
@@ -76,7 +106,7 @@ int main() {
     float ms; (void)hipEventElapsedTime(&ms, e0, e1);
     (void)hipMemcpy(hc.data(), cyc, 256 * WAVES * 8, hipMemcpyDeviceToHost);
     double m = 0; for (auto c : hc) m += c; m /= hc.size();
-    if (rep == 3) printf("split chain: %.0f cycles/layer (MFMA-bound %d), %.3f ms\n", m / (TILES * 5.0), 32 * kTerms * 32, ms);
+    if (rep == 3) printf("split chain: %.0f cycles/layer per wave (tile-layers %d per wave; MFMA-bound %d per tile-layer), %.3f ms\n", m / (TILES * 5.0), TILES * 5, 32 * kTerms * 32, ms);
   }
   return 0;
 }
