@@ -231,6 +231,18 @@ __device__ __forceinline__ auto& pick(A& a, B& b) {
 #ifdef ECNF_SPLIT_WLDS
 __shared__ unsigned g_wlds_exp[8 * kPieces * 256];
 #endif
+#ifdef ECNF_SPLIT_RING
+// experiment: a workgroup-shared LDS ring of weight fragments.  Every wave runs the same chain in lockstep; the
+// segment's groups are streamed in intervals of RIV groups, double-buffered: during interval i each wave loads its
+// share of interval i + 1's pieces from global memory into registers and writes them to the other half at the end
+// of the interval, then a workgroup barrier publishes them.  One global fetch per piece per workgroup instead of
+// one per wave; the waves read the fragments from LDS (2 ds_read_b128 per group).
+#ifndef ECNF_RING_IV
+#define ECNF_RING_IV 4
+#endif
+constexpr int kRingIV = ECNF_RING_IV;
+__shared__ unsigned g_ring[2 * kRingIV * kPieces * 256];
+#endif
 // NT = 1 (forward-mode tangent, the divergence kernels): XAT / XBT / accT carry the tangent of every activation
 // through the same layers.  Each weight fragment feeds 2 kTerms MFMAs (primal and tangent interleaved); the
 // tangent of a layer is du = accT inv (no bias) and dy' = silu'(t) du = r (1 - ln2 u (1 - r)) du with the primal's
@@ -251,10 +263,43 @@ __device__ __forceinline__ void chain_split(SplitX<NF>& XA, SplitX<NF>& XB, f32x
                                                                          0x7fffffff, 0x00020000);
   const int voff = lane * 16;
   u32x4 wbuf[PF + 1][kPieces];
+#ifdef ECNF_SPLIT_RING
+  static_assert(G % kRingIV == 0, "segment groups must fill whole ring intervals");
+  const int rwave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), rnw = blockDim.x >> 6;
+  constexpr int kIvPieces = kRingIV * kPieces;
+  // this wave's pieces of an interval: q = rwave, rwave + rnw, ... (< kIvPieces); at most 2 per wave (rnw >= 4)
+  u32x4 rnext[2];
+  auto ring_fetch = [&](int iv) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int q = rwave + k * rnw;
+      if (q < kIvPieces) rnext[k] = wload(rsrc, voff, (iv * kIvPieces + q) * kPieceBytes);
+    }
+  };
+  auto ring_store = [&](int iv) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int q = rwave + k * rnw;
+      if (q < kIvPieces) *reinterpret_cast<u32x4*>(g_ring + (((iv & 1) * kIvPieces + q) * 256 + lane * 4)) = rnext[k];
+    }
+  };
+  auto ring_read = [&](int gg, u32x4 (&w)[kPieces]) {
+#pragma unroll
+    for (int p = 0; p < kPieces; ++p)
+      w[p] = *reinterpret_cast<const u32x4*>(g_ring + (((((gg / kRingIV) & 1) * kRingIV + gg % kRingIV) * kPieces + p) * 256 +
+                                                       lane * 4));
+  };
+  ring_fetch(0);
+  ring_store(0);
+  __syncthreads();
+  if (kRingIV < G) ring_fetch(1);
+  ring_read(0, wbuf[0]);
+#else
 #pragma unroll
   for (int gg = 0; gg < PF && gg < G; ++gg)
 #pragma unroll
     for (int p = 0; p < kPieces; ++p) wbuf[gg][p] = wload(rsrc, voff, (gg * kPieces + p) * kPieceBytes);
+#endif
   // per-item pipeline registers (SSA after unrolling: only live items occupy registers)
   f32x2 bv[NI], uv[NI], ev[NI], dv[NI], e2v[NI];
 #ifdef ECNF_CHAIN_BIAS_INIT
@@ -292,7 +337,10 @@ __device__ __forceinline__ void chain_split(SplitX<NF>& XA, SplitX<NF>& XB, f32x
 #else
     constexpr int nbias = Plan::count(gg + 1, 0);
 #endif
-#if defined(ECNF_SPLIT_WLDS)   // timing experiment: fragments from an LDS image of 8 groups (g_wlds_exp)
+#if defined(ECNF_SPLIT_RING)
+    // next group's fragments from the ring, unless the next group opens a new interval (read after the barrier)
+    if constexpr (gg + 1 < G && (gg + 1) % kRingIV != 0) ring_read(gg + 1, wbuf[(gg + 1) % (PF + 1)]);
+#elif defined(ECNF_SPLIT_WLDS)   // timing experiment: fragments from an LDS image of 8 groups (g_wlds_exp)
     if constexpr (gg + PF < G) {
 #pragma unroll
       for (int p = 0; p < kPieces; ++p)
@@ -496,6 +544,17 @@ __device__ __forceinline__ void chain_split(SplitX<NF>& XA, SplitX<NF>& XB, f32x
       });
 #endif
       __builtin_amdgcn_sched_barrier(0);
+    }
+#endif
+#ifdef ECNF_SPLIT_RING
+    if constexpr (mfma_group && gg % kRingIV == kRingIV - 1) {
+      constexpr int iv = gg / kRingIV;
+      if constexpr ((iv + 1) * kRingIV < G) {
+        ring_store(iv + 1);
+        __syncthreads();
+        if constexpr ((iv + 2) * kRingIV < G) ring_fetch(iv + 2);
+        ring_read(gg + 1, wbuf[(gg + 1) % (PF + 1)]);
+      }
     }
 #endif
   });

@@ -2,7 +2,7 @@
 # Build (no arg) or run (arg "run") the split-chain microbenchmark variants tools/micro/sb_<name>.
 # Variants: waves per CU (1 or 2 per SIMD) x {production, cheap activation, no weight loads, no transcendentals}.
 D="$(cd "$(dirname "$0")" && pwd)"
-V="w4:-DWAVES=4 w8:-DWAVES=8 w4two:-DWAVES=4|-DTWO_TILES w4twonowl:-DWAVES=4|-DTWO_TILES|-DECNF_SPLIT_NO_WLOAD w8nowl:-DWAVES=8|-DECNF_SPLIT_NO_WLOAD"
+V="w8:-DWAVES=8 w8ring:-DWAVES=8|-DECNF_SPLIT_RING w8ring8:-DWAVES=8|-DECNF_SPLIT_RING|-DECNF_RING_IV=8 w8ring2:-DWAVES=8|-DECNF_SPLIT_RING|-DECNF_RING_IV=2 w8wlds:-DWAVES=8|-DECNF_SPLIT_WLDS"
 if [ "$1" = "run" ]; then
   for v in $V; do n=${v%%:*}; echo -n "$n: "; timeout -k 5 60 "$D/sb_$n" || exit 1; done
   exit 0
