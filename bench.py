@@ -85,6 +85,68 @@ def roofline_peak(cfg, chain_mode: str) -> float:
     return F / ((F - Fv) / p_split + Fv / PEAK_FP32_MFMA_TFLOPS)
 
 
+class ClockSampler:
+    """Samples the shader clock (the current level of the device's sysfs pp_dpm_sclk) and the board power (hwmon) of
+    OUR device (matched by PCI address) on a host thread while the timed region runs.  The split-fp16 MFMA-dense
+    kernel does not hold 2.4 GHz, so the roofline also reports the fraction at the sampled clock.
+    Returns None fields when sysfs is not readable."""
+
+    def __init__(self, dev):
+        import glob
+        import threading
+        self.card = None
+        try:
+            import torch
+            p = torch.cuda.get_device_properties(dev)
+            bus = f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}"
+            for c in glob.glob("/sys/class/drm/card*/device"):
+                if os.path.basename(os.path.realpath(c)).startswith(bus):
+                    self.card = c
+                    break
+        except Exception:
+            self.card = None
+        self.sclk, self.power = [], []
+        self._stop = threading.Event()
+        self._t = threading.Thread(target=self._run, daemon=True)
+
+    def _read(self):
+        with open(os.path.join(self.card, "pp_dpm_sclk")) as f:
+            for line in f:
+                if line.rstrip().endswith("*"):
+                    self.sclk.append(float(line.split(":")[1].strip().rstrip("*").strip().lower().rstrip("mhz")))
+        import glob
+        for pf in glob.glob(os.path.join(self.card, "hwmon", "hwmon*", "power1_*")):
+            if pf.endswith(("power1_average", "power1_input")):
+                with open(pf) as f:
+                    self.power.append(float(f.read()) / 1e6)
+                break
+
+    def _run(self):
+        while not self._stop.is_set():
+            try:
+                self._read()
+            except Exception:
+                return
+            time.sleep(0.002)
+
+    def __enter__(self):
+        if self.card:
+            self._t.start()
+        return self
+
+    def __exit__(self, *exc):
+        self._stop.set()
+        if self.card:
+            self._t.join(timeout=1.0)
+
+    def summary(self):
+        import statistics
+        return {"sclk_mhz_median": statistics.median(self.sclk) if self.sclk else None,
+                "power_w_median": statistics.median(self.power) if self.power else None,
+                "samples": len(self.sclk),
+                "source": "sysfs pp_dpm_sclk / hwmon of the device's PCI address, sampled every 2 ms in the timed region"}
+
+
 def cpu_model() -> str:
     try:
         out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=20).stdout
@@ -224,14 +286,16 @@ def main():
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     barrier()
     torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        ev[i][0].record(stream)
-        y1, _, nfe, status = step()
-        ev[i][1].record(stream)
-    torch.cuda.synchronize(dev)
+    with ClockSampler(local) as clock:
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            ev[i][0].record(stream)
+            y1, _, nfe, status = step()
+            ev[i][1].record(stream)
+        torch.cuda.synchronize(dev)
+        t_run = time.perf_counter() - t0
     barrier()
-    t_max = max_over_ranks(time.perf_counter() - t0)
+    t_max = max_over_ranks(t_run)
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev])) if args.steps else 0.0
     assert int((status != 0).sum()) == 0 and torch.isfinite(y1).all()
 
@@ -356,6 +420,9 @@ def main():
                          "flop_basis": "live dense-contraction FLOPs per EGNN eval (SURVEY 8d F minus the last "
                                        "block's dead h update) x NFE x batch",
                          "frac_vs_fp32_mfma_peak": achieved / PEAK_FP32_MFMA_TFLOPS,
+                         "device_clock": clock.summary(),
+                         "frac_at_sampled_sclk": (achieved / (peak * clock.summary()["sclk_mhz_median"] / 2400.0)
+                                                  if clock.summary()["sclk_mhz_median"] else None),
                          "peak_basis": (f"GEMM FLOPs at the dense 16-bit MFMA peak / {SPLIT_TERMS[chain_mode]} split "
                                         "terms, vector FLOPs at the fp32 peak") if chain_mode in SPLIT_TERMS
                                        else "fp32 MFMA peak"},
