@@ -210,6 +210,12 @@ struct ChainInv {
 #ifndef ECNF_SPLIT_PF
 #define ECNF_SPLIT_PF 3
 #endif
+// the activation's stage-B add and stage-C multiply as packed fp32 (v_pk_add_f32 / v_pk_mul_f32) where the compiler
+// keeps the pair in an aligned register pair (bit-identical; LJ13 27.14 -> 27.02 ms A/B, profiles/round2/e3);
+// -DECNF_SPLIT_NO_PK: scalar
+#if !defined(ECNF_SPLIT_NO_PK) && !defined(ECNF_SPLIT_PK)
+#define ECNF_SPLIT_PK 1
+#endif
 
 __device__ __forceinline__ u32x4 wload(__amdgpu_buffer_rsrc_t rsrc, int voff, int soff) {
 #ifdef ECNF_SPLIT_WLOAD_SAME   // timing experiment: every group reads the first group's fragments (L1-resident)
@@ -437,6 +443,12 @@ __device__ __forceinline__ void chain_split(SplitX<NF>& XA, SplitX<NF>& XB, f32x
 #elif defined(ECNF_SPLIT_NO_TRANS)
       ev[id][0] = 0.25f * (1.0f + ev[id][0]);
       ev[id][1] = 0.25f * (1.0f + ev[id][1]);
+#elif defined(ECNF_SPLIT_PK)
+      {
+        const f32x2 s = ev[id] + 1.0f;   // v_pk_add_f32: one issue for the pair
+        ev[id][0] = __builtin_amdgcn_rcpf(s[0]);
+        ev[id][1] = __builtin_amdgcn_rcpf(s[1]);
+      }
 #else
       ev[id][0] = __builtin_amdgcn_rcpf(1.0f + ev[id][0]);
       ev[id][1] = __builtin_amdgcn_rcpf(1.0f + ev[id][1]);
@@ -452,6 +464,9 @@ __device__ __forceinline__ void chain_split(SplitX<NF>& XA, SplitX<NF>& XB, f32x
       constexpr typename Plan::Item it = Plan::item(id);
 #ifdef ECNF_SPLIT_IDENT_ACT
       const float y0 = uv[id][0], y1 = uv[id][1];
+#elif defined(ECNF_SPLIT_PK)
+      const f32x2 yv = uv[id] * ev[id];   // v_pk_mul_f32
+      const float y0 = yv[0], y1 = yv[1];
 #else
       const float y0 = uv[id][0] * ev[id][0];
       const float y1 = uv[id][1] * ev[id][1];
@@ -474,8 +489,14 @@ __device__ __forceinline__ void chain_split(SplitX<NF>& XA, SplitX<NF>& XB, f32x
       } else if constexpr (NT) {
         constexpr float kNegLn2 = -0.69314718055994531f;
         // u (1 - r) = u - y' (y' = u r): 4 VALU per element instead of 5
+#ifdef ECNF_SPLIT_PK
+        const f32x2 dd = (ev[id] * dv[id]) * __builtin_elementwise_fma(uv[id] - (f32x2){y0, y1}, (f32x2)kNegLn2,
+                                                                      (f32x2)1.0f);
+        const float d0 = dd[0], d1 = dd[1];
+#else
         const float d0 = ev[id][0] * dv[id][0] * fmaf(uv[id][0] - y0, kNegLn2, 1.0f);
         const float d1 = ev[id][1] * dv[id][1] * fmaf(uv[id][1] - y1, kNegLn2, 1.0f);
+#endif
         if constexpr (it.l < NL - 1) {
           put_pair<NF, it.j, 2 * it.p>(pick<(it.l + 1) & 1>(XAT, XBT), d0, d1);
         } else {

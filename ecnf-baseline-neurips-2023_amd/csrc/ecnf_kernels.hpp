@@ -133,7 +133,7 @@ enum Phase { kEuler = 0, kInit0 = 1, kInit1 = 2, kFsal = 3, kStage = 4 };
 
 // The whole solve as a phase machine around ONE field evaluation per loop trip.
 template <int NF, int NT, int L, int D, int P>
-__global__ __launch_bounds__((Geo<NF, NT, P>::NTHR)) void integrate_kernel(Net net, SolveP sp, const float* __restrict__ y0,
+__global__ __launch_bounds__((Geo<NF, NT, P>::NTHR)) __attribute__((amdgpu_waves_per_eu(Geo<NF, NT, P>::WPE))) void integrate_kernel(Net net, SolveP sp, const float* __restrict__ y0,
                                                                   const int32_t* __restrict__ feat,
                                                                   const float* __restrict__ eps, float* y1,
                                                                   float* dlogp, int32_t* nfe_out,
@@ -385,7 +385,7 @@ __global__ __launch_bounds__((Geo<NF, NT, P>::NTHR)) void integrate_kernel(Net n
 
 // one evaluation (and n_tangents JVPs) per molecule
 template <int NF, int NT, int L, int D, int P>
-__global__ __launch_bounds__((Geo<NF, NT, P>::NTHR)) void vf_kernel(Net net, const float* __restrict__ x,
+__global__ __launch_bounds__((Geo<NF, NT, P>::NTHR)) __attribute__((amdgpu_waves_per_eu(Geo<NF, NT, P>::WPE))) void vf_kernel(Net net, const float* __restrict__ x,
                                                            const float* __restrict__ t,
                                                            const int32_t* __restrict__ feat,
                                                            const float* __restrict__ tan_in, int ntan, float* v,

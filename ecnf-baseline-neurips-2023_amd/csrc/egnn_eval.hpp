@@ -83,6 +83,9 @@ struct Geo {
 #endif
   static constexpr int NW = (NT == 0 && NF <= 4) ? (kSplit ? ECNF_SPLIT_NW : 8) : 4;
   static constexpr int NTHR = 64 * NW;
+  // minimum waves per SIMD the register allocation must allow (2 x 4-wave workgroups per CU for the split primal
+  // kernels at -DECNF_SPLIT_NW=4)
+  static constexpr int WPE = (kSplit && NW == 4) ? 2 : 1;
 };
 constexpr int kMaxBlocks = 10;
 constexpr int kMaxPhiH = 5;     // L + 1 <= 5

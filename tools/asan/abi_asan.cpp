@@ -18,8 +18,11 @@
 #include "ecnf.h"
 
 static int g_fail = 0;
+// ABI_ASAN_TRACE=1: print each check's line (stderr) before it runs, so a stall names its call
+static const bool g_trace = std::getenv("ABI_ASAN_TRACE") != nullptr;
 #define CHECK(cond, ...)                                                   \
   do {                                                                     \
+    if (g_trace) std::fprintf(stderr, "check line %d\n", __LINE__);       \
     if (!(cond)) {                                                         \
       std::fprintf(stderr, "FAIL %s:%d: %s: ", __FILE__, __LINE__, #cond); \
       std::fprintf(stderr, __VA_ARGS__);                                   \
@@ -180,7 +183,10 @@ int main() {
   const ecnf_cfg cfgs[] = {make_cfg(4, 2, 1, 64, 128, 3, 3, 1.f), make_cfg(13, 3, 1, 64, 128, 3, 3, 1.f),
                            make_cfg(22, 3, 22, 32, 64, 2, 3, 0.2f), make_cfg(29, 3, 1, 32, 256, 4, 5, 2.f)};
   int gpu = 0;
-  for (const auto& c : cfgs) gpu += device_checks(c, 5) ? 1 : 0;
+  for (const auto& c : cfgs) {
+    if (g_trace) std::fprintf(stderr, "config N = %d, M = %d\n", c.n_nodes, c.mlp_width);
+    gpu += device_checks(c, 5) ? 1 : 0;
+  }
   std::printf("abi_asan: %s, %d failure(s)\n", gpu ? "host + device paths" : "host paths only (no GPU)", g_fail);
   return g_fail ? 1 : 0;
 }

@@ -34,6 +34,9 @@ res = {os.path.basename(l)[5:-3]: [] for l in libs}
 for r in range(rounds):
     for lib in libs:
         env = dict(os.environ, ECNF_LIB=lib)
+        envf = lib[:-3] + ".env"   # optional KEY=VALUE lines for this library (e.g. ECNF_MPW)
+        if os.path.exists(envf):
+            env.update(dict(l.strip().split("=", 1) for l in open(envf) if "=" in l))
         out = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True, timeout=120)
         if out.returncode != 0:
             print(out.stderr[-2000:])
