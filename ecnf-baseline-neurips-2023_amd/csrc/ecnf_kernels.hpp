@@ -90,10 +90,17 @@ __device__ __forceinline__ void joint_field(const Net& net, const Lds& s, const 
                                             float* kx_out, float* kl_out) {
   constexpr int kThreads = Geo<NF, NT, P>::NTHR;
   const int tid = opaque_tid(), MPW = net.MPW, ND = net.ND;
-  // NT == 0: one primal eval; Hutchinson: one JVP along eps; exact: ND JVPs along e_k (trace of J)
-  const int nrep = (NT == 0 || sp.div == ECNF_DIV_HUTCHINSON) ? 1 : ND;
-  if (tid < MPW) st.divv[tid] = 0.f;
-  for (int k = 0; k < nrep; ++k) {
+  // NT == 0: one primal eval; Hutchinson: one JVP along eps; exact: the trace of J from ND - D JVPs along e_k,
+  // k >= D.  The field only sees relative positions and subtracts the input mean (egnn.py:176-188), so
+  // v(x + s 1) = v(x) - s exactly, i.e. J T_c = -T_c for the translations T_c = sum_a e_(a,c).  In the basis
+  // {T_c} u {e_k, k >= D} the dual vectors are e_(0,c) and e_k - e_(k mod D), hence
+  //   tr J = sum_{k >= D} (J_kk - J_(k mod D),k) - D
+  // with J_(k mod D),k the atom-0 component of the same JVP column (D fewer evaluations than the ND unit JVPs).
+  const bool exact = NT && sp.div != ECNF_DIV_HUTCHINSON;
+  const int nrep = exact ? ND - D : 1;
+  if (tid < MPW) st.divv[tid] = exact ? -(float)D : 0.f;
+  for (int k0 = 0; k0 < nrep; ++k0) {
+    const int k = exact ? k0 + D : k0;
     if constexpr (NT) {
       if (sp.div == ECNF_DIV_HUTCHINSON) {
         for (int i = tid; i < MPW * ND; i += kThreads) st.tin[i] = st.eps[i];
@@ -110,7 +117,7 @@ __device__ __forceinline__ void joint_field(const Net& net, const Lds& s, const 
           for (int c = 0; c < ND; ++c) acc += st.tout[tid * ND + c] * st.eps[tid * ND + c];
           st.divv[tid] = acc;
         } else {
-          st.divv[tid] += st.tout[tid * ND + k];
+          st.divv[tid] += st.tout[tid * ND + k] - st.tout[tid * ND + k % D];
         }
       }
     }

