@@ -109,7 +109,7 @@ __device__ __forceinline__ void joint_field(const Net& net, const Lds& s, const 
       }
       __syncthreads();
     }
-    egnn_eval<NF, NT, L, D, P>(net, s, st.ys, st.ts, st.tin, st.vout, st.tout);
+    egnn_eval<NF, NT, L, D, P>(net, s, st.ys, st.ts, st.tin, st.vout, st.tout, st.active);
     if constexpr (NT) {
       if (tid < MPW) {
         if (sp.div == ECNF_DIV_HUTCHINSON) {

@@ -83,9 +83,10 @@ struct Geo {
 #endif
   static constexpr int NW = (NT == 0 && NF <= 4) ? (kSplit ? ECNF_SPLIT_NW : 8) : 4;
   static constexpr int NTHR = 64 * NW;
-  // minimum waves per SIMD the register allocation must allow (2 x 4-wave workgroups per CU for the split primal
-  // kernels at -DECNF_SPLIT_NW=4)
-  static constexpr int WPE = (kSplit && NW == 4) ? 2 : 1;
+  // minimum waves per SIMD the register allocation must allow: 2 only for 2 x 4-wave workgroups per CU of the M <= 128
+  // split primal kernels at -DECNF_SPLIT_NW=4.  (The M = 256 split primal kernels also run 4 waves, but need their
+  // 512 registers: at 2 waves per SIMD they spilled 968 B per lane and QM9 B = 2048 Euler-100 ran 2162 -> 3423 ms.)
+  static constexpr int WPE = (kSplit && NF <= 4 && NW == 4) ? 2 : 1;
 };
 constexpr int kMaxBlocks = 10;
 constexpr int kMaxPhiH = 5;     // L + 1 <= 5
@@ -1344,7 +1345,7 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
 // ---------------------------------------------------------------------------------------------------
 template <int NF, int NT, int L, int D, int P>
 __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const float* x_in, const float* t_in, const float* tan_in,
-                          float* v_out, float* tan_out) {
+                          float* v_out, float* tan_out, const int* act = nullptr) {
   constexpr int kNW = Geo<NF, NT, P>::NW, kNT = Geo<NF, NT, P>::NTHR;
   constexpr bool kSplitG = Geo<NF, NT, P>::kSplit;
   constexpr bool kSplitN = Geo<NF, NT, P>::kSplitN;   // split node GEMMs (primal split kernels and tangent kernels)
@@ -1434,10 +1435,37 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
 #else
     const int ntiles_run = ntiles;
 #endif
+#ifdef ECNF_EXP_BALANCED
     {
       const int elane = opaque_tid() & 63;
       for (int tile = wave; tile < ntiles_run; tile += kNW) edge_tile<NF, NT, L, D, P>(net, bw, s, tile, elane, need_h);
     }
+#else
+    {
+      // act (LDS [MPW], the solver's per-molecule flags; nullptr = every slot): the edge tiles of molecules whose
+      // adaptive solve has finished, and of slots that pad the last workgroup, are skipped and the remaining tiles
+      // are dealt round-robin over the waves, so a workgroup's tail after its faster molecules finish runs at the
+      // cost of the molecules still integrating.  Skipped molecules' outputs are never committed; every molecule's
+      // tiles and node rows are its own, so the others' results are unchanged (bitwise).
+      const int elane = opaque_tid() & 63;
+      const int tpm = net.EP >> 5;
+      unsigned amask = MPW >= 32 ? 0xffffffffu : (1u << MPW) - 1u;
+      if (act) {
+        amask = 0;
+        for (int m = 0; m < MPW; ++m) amask |= (act[m] != 0 ? 1u : 0u) << m;
+      }
+      amask = __builtin_amdgcn_readfirstlane(amask);
+      (void)ntiles_run;
+      const int nrun = __builtin_popcount(amask) * tpm;
+      for (int vt = wave; vt < nrun; vt += kNW) {
+        const int q = vt / tpm;
+        unsigned mm = amask;
+        for (int i = 0; i < q; ++i) mm &= mm - 1u;   // drop the q lowest active molecules
+        const int tile = __builtin_ctz(mm) * tpm + (vt - q * tpm);
+        edge_tile<NF, NT, L, D, P>(net, bw, s, tile, elane, need_h);
+      }
+    }
+#endif
     __syncthreads();
     STAMP(s, kStEdge);
     tid = opaque_tid();

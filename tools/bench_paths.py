@@ -66,7 +66,9 @@ def run_case(name, B, solver, step, div, direction):
     rec = {"config": name, "batch": B, "solver": solver, "step": step, "divergence": div, "direction": direction,
            "ms": round(ms, 3), "molecules_per_s": round(B / ms * 1e3, 1), "nfe_mean": round(nfe_mean, 2),
            "tflops": round(flop / ms / 1e9, 2), "bad_status": int((st != 0).sum()),
-           "finite": bool(torch.isfinite(y1).all())}
+           "finite": bool(torch.isfinite(y1).all()),
+           # checksums for A/B runs of two libraries (equal sums: the outputs did not change)
+           "y_sum": float(y1.double().abs().sum()), "dl_sum": float(dl.double().abs().sum()) if dl is not None else 0.0}
     h.close()
     return rec
 
