@@ -946,6 +946,14 @@ int ecnf_integrate(ecnf_handle* h, const ecnf_solve_opts* o, const float* y0, co
   sp.rtol = o->rtol;
   sp.atol = o->atol;
   sp.dtmin = o->dtmin;
+  // exact trace: block 1's sparse dual tiles (egnn_eval sparse_a) where a molecule has >= 3 edge tiles per dual tile
+  // (LJ13: 5 vs 1, ALDP: 15 vs 2; not DW4: 1 vs 1); kernels other than the M <= 128 split tangent kernels ignore it.
+  // ECNF_EXACT_SPARSE=0 turns it off (A/B and parity tests)
+  {
+    const int nn1 = h->cfg.n_nodes - 1, tpm = (h->cfg.n_nodes * nn1 + 31) / 32, ndt = (2 * nn1 + 31) / 32;
+    const char* env = std::getenv("ECNF_EXACT_SPARSE");
+    sp.sparse1 = (o->divergence == ECNF_DIV_EXACT && tpm >= 3 * ndt && !(env && std::atoi(env) == 0)) ? 1 : 0;
+  }
   HIP_TRY(hipSetDevice(h->device));
   HIP_TRY(dispatch_integrate(h, NT, sp, y0, feat, eps, y1, dlogp, nfe, status, batch, (hipStream_t)stream));
   g_err.clear();

@@ -39,6 +39,10 @@ __constant__ float kBerr[7] = {(float)(35.0 / 384 - 1951.0 / 21600),
 struct SolveP {
   int solver, div, adaptive, max_steps;
   float tau0, tau1, dirf, dt0, rtol, atol, dtmin;
+  // exact trace: block 1 runs the edges at the tangent's atom as dual tiles and every edge as a primal tile
+  // (egnn_eval sparse_a; set by the host where it pays: the M <= 128 split tangent kernels, >= 3 tiles per molecule
+  // per dual tile)
+  int sparse1;
 };
 
 // solver state in LDS, after the eval region
@@ -109,7 +113,10 @@ __device__ __forceinline__ void joint_field(const Net& net, const Lds& s, const 
       }
       __syncthreads();
     }
-    egnn_eval<NF, NT, L, D, P>(net, s, st.ys, st.ts, st.tin, st.vout, st.tout, st.active);
+    // exact: the unit tangent e_k sits on atom k / D, so block 1 (whose node features carry no tangent) has nonzero
+    // edge tangents only on the 2(N - 1) edges at that atom
+    egnn_eval<NF, NT, L, D, P>(net, s, st.ys, st.ts, st.tin, st.vout, st.tout, st.active,
+                               exact && sp.sparse1 ? k / D : -1);
     if constexpr (NT) {
       if (tid < MPW) {
         if (sp.div == ECNF_DIV_HUTCHINSON) {

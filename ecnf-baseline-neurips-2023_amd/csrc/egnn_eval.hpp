@@ -872,7 +872,7 @@ template <int NF, int NT, int L, int D>
 __device__ __forceinline__ void edge_shift(const Net& net, const BlockW& bw, const Lds& s, const f32x16 (&px)[NF],
                                            const f32x16 (&pxT)[NF], bool writer, const SegScan& sc, int rr,
                                            const float (&r)[D], const float (&dr)[D], float length, float dlength,
-                                           int lane) {
+                                           int lane, bool pw = true) {
   const int kk = lane >> 5;
   float phx = 0.f, phxT = 0.f;
 #pragma unroll
@@ -901,18 +901,20 @@ __device__ __forceinline__ void edge_shift(const Net& net, const BlockW& bw, con
   if (writer && kk == 0) {
 #pragma unroll
     for (int d = 0; d < D; ++d) {
-      lds_add(&s.dxacc[rr * D + d], sh[d]);
+      if (pw) lds_add(&s.dxacc[rr * D + d], sh[d]);
       if constexpr (NT) lds_add(&s.dxacc[(RP + rr) * D + d], sh[D + d]);
     }
   }
 }
 
-// gate, message aggregation, phi_x torso + output, shifts (egnn.py:81-104); `m` holds the messages
+// gate, message aggregation, phi_x torso + output, shifts (egnn.py:81-104); `m` holds the messages.
+// pw = false: the tile's primal outputs are computed (the tangents need them) but not stored (exact-trace block-1
+// dual tiles, whose edges' primal contributions come from the primal tiles)
 template <int NF, int NT, int L, int D, typename PhiX>
 __device__ __forceinline__ void edge_tail(const Net& net, const BlockW& bw, const Lds& s, f32x16 (&X)[NF],
                                           f32x16 (&XT)[NF], bool valid, int rr, float* agg_dst,
                                           const float (&r)[D], const float (&dr)[D], float length, float dlength,
-                                          int lane, bool agg, PhiX&& phi_x) {
+                                          int lane, bool agg, PhiX&& phi_x, bool pw = true) {
   f32x16(&m)[NF] = X;
   f32x16(&mT)[NF] = XT;
   const int kk = lane >> 5, li = lane & 31;
@@ -950,7 +952,7 @@ __device__ __forceinline__ void edge_tail(const Net& net, const BlockW& bw, cons
 #ifndef ECNF_EXP_NO_AGG
     sc.sum_many<16, true>(v);
 #endif
-    if (writer) {
+    if (writer && pw) {
       if (agg_dst) {
         // the segment part's sums as 4 x 16-B stores into its own row (no atomics; combined in the node update)
 #pragma unroll
@@ -978,7 +980,7 @@ __device__ __forceinline__ void edge_tail(const Net& net, const BlockW& bw, cons
   // phi_x torso (egnn.py:82) then its Dense(1) and the shifts
   phi_x(X, XT);
 #ifndef ECNF_EXP_NO_SHIFT
-  edge_shift<NF, NT, L, D>(net, bw, s, X, XT, writer, sc, rr, r, dr, length, dlength, lane);
+  edge_shift<NF, NT, L, D>(net, bw, s, X, XT, writer, sc, rr, r, dr, length, dlength, lane, pw);
 #endif
 }
 
@@ -1068,8 +1070,12 @@ __device__ __forceinline__ void edge_layer1_dual(const Net& net, const BlockW& b
 }
 
 // one 32-edge tile through phi_e / gate / phi_x  (egnn.py:72-95)
+// a >= 0 (split tangent kernels only, exact trace, block 1): `tile` is a molecule and the tile is dual tile `part`
+// of the 2(N - 1) edges at atom a of that molecule, in receiver-major order (receivers i < a with sender a, then
+// receiver a with its N - 1 senders in graph.py order, then receivers i > a), storing tangent outputs only
 template <int NF, int NT, int L, int D, int P>
-__device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, const Lds& s, int tile, int lane, bool agg) {
+__device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, const Lds& s, int tile, int lane, bool agg,
+                                          int a = -1, int part = 0) {
   const int kk = lane >> 5, li = lane & 31;
 #ifdef ECNF_EXP_CHAIN_ONLY
   {  // timing experiment: the two chain segments alone, on synthetic activations, one LDS add as the sink
@@ -1091,16 +1097,38 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
   }
 #endif
   const int N = net.N, E = net.E, nn1 = N - 1, RP = net.RP, M = NF * 32;
-  // each molecule owns EP = 32*ceil(E/32) edge slots, so its tiles (and every rounding inside them) do not
-  // depend on which slot of the workgroup, i.e. which batch position, it occupies
-  const int mol = (tile * 32) / net.EP;
-  const int e_in = tile * 32 + li - mol * net.EP;
-  const bool valid = (mol < net.MPW) && (e_in < E);
-  const int el = valid ? e_in : 0;
-  const int i = el / nn1;
-  const int jj = el - i * nn1;
-  int sd = i + 1 + jj;
-  if (sd >= N) sd -= N;
+  int mol, i, sd;
+  bool valid;
+  if (a < 0) {
+    // each molecule owns EP = 32*ceil(E/32) edge slots, so its tiles (and every rounding inside them) do not
+    // depend on which slot of the workgroup, i.e. which batch position, it occupies
+    mol = (tile * 32) / net.EP;
+    const int e_in = tile * 32 + li - mol * net.EP;
+    valid = (mol < net.MPW) && (e_in < E);
+    const int el = valid ? e_in : 0;
+    i = el / nn1;
+    sd = i + 1 + (el - i * nn1);
+    if (sd >= N) sd -= N;
+  } else {
+    ECNF_DCHECK((Geo<NF, NT, P>::kL2T && tile < net.MPW && a < N), 6);
+    mol = tile;
+    const int q = part * 32 + li;
+    valid = q < 2 * nn1;
+    if (q < a) {
+      i = q;
+      sd = a;
+    } else if (q < a + nn1) {   // receiver a, sender (a + 1 + j) mod N with j = q - a
+      i = a;
+      sd = q + 1 < N ? q + 1 : q + 1 - N;
+    } else {
+      i = q - nn1 + 1;
+      sd = a;
+    }
+    if (!valid) {
+      i = 0;
+      sd = 1;
+    }
+  }
   const int mrow = valid ? mol : 0;
   const int rr = mrow * N + i, rs = mrow * N + sd;   // receiver / sender rows (graph.py:10-13)
   ECNF_DCHECK(rr < net.MPW * N && rs < net.MPW * N && rr >= 0 && rs >= 0, 1);
@@ -1257,7 +1285,8 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
                                 });
                               });
                               chain_split<NF, L, 1>(XA, XB, Y, Wx, s.vecs + (L - 1) * NF * 32, ix, lane, XAT, XBT, YT);
-                            });
+                            },
+                            a < 0);   // block-1 dual tiles of the exact trace store tangents only
     STAMP_LANE0(s, kStEdgeTail, t_sub);
     return;
   }
@@ -1345,7 +1374,7 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
 // ---------------------------------------------------------------------------------------------------
 template <int NF, int NT, int L, int D, int P>
 __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const float* x_in, const float* t_in, const float* tan_in,
-                          float* v_out, float* tan_out, const int* act = nullptr) {
+                          float* v_out, float* tan_out, const int* act = nullptr, int sparse_a = -1) {
   constexpr int kNW = Geo<NF, NT, P>::NW, kNT = Geo<NF, NT, P>::NTHR;
   constexpr bool kSplitG = Geo<NF, NT, P>::kSplit;
   constexpr bool kSplitN = Geo<NF, NT, P>::kSplitN;   // split node GEMMs (primal split kernels and tangent kernels)
@@ -1456,12 +1485,38 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
       }
       amask = __builtin_amdgcn_readfirstlane(amask);
       (void)ntiles_run;
-      const int nrun = __builtin_popcount(amask) * tpm;
-      for (int vt = wave; vt < nrun; vt += kNW) {
-        const int q = vt / tpm;
+      const int nact = __builtin_popcount(amask);
+      auto nth_active = [&](int q) {
         unsigned mm = amask;
         for (int i = 0; i < q; ++i) mm &= mm - 1u;   // drop the q lowest active molecules
-        const int tile = __builtin_ctz(mm) * tpm + (vt - q * tpm);
+        return __builtin_ctz(mm);
+      };
+      // exact trace, block 1 (sparse_a = the unit tangent's atom): h carries no tangent yet (embedding and time
+      // only), so an edge's tangent is nonzero only if it touches atom a (dr = 0 otherwise, and the chains, gate
+      // and shift of a zero input tangent are exactly zero).  Every edge runs as a primal tile and the 2(N - 1)
+      // edges at a as dual tiles storing tangents only: per molecule tpm primal + ceil(2(N - 1) / 32) dual tiles
+      // instead of tpm dual tiles (the dual tiles are dealt first)
+      int ndt = 0;
+      if constexpr (Geo<NF, NT, P>::kL2T)
+        if (sparse_a >= 0 && k == 0) ndt = (2 * (N - 1) + 31) >> 5;
+      const int nd = nact * ndt;
+      const int nrun = nd + nact * tpm;
+      for (int vt = wave; vt < nrun; vt += kNW) {
+        if constexpr (Geo<NF, NT, P>::kL2T) {
+          if (vt < nd) {
+            const int q = vt / ndt;
+            edge_tile<NF, NT, L, D, P>(net, bw, s, nth_active(q), elane, need_h, sparse_a, vt - q * ndt);
+            continue;
+          }
+        }
+        const int v2 = vt - nd, q = v2 / tpm;
+        const int tile = nth_active(q) * tpm + (v2 - q * tpm);
+        if constexpr (Geo<NF, NT, P>::kL2T) {
+          if (ndt) {
+            edge_tile<NF, 0, L, D, P>(net, bw, s, tile, elane, need_h);
+            continue;
+          }
+        }
         edge_tile<NF, NT, L, D, P>(net, bw, s, tile, elane, need_h);
       }
     }

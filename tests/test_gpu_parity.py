@@ -8,6 +8,8 @@ Tolerances (fp32 kernel vs fp64 oracle; stated per test):
     batch-mean NFE within 30 % of the oracle's
   * log-densities: |err| <= 2e-3 absolute (values are O(10-100))
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -230,6 +232,34 @@ def test_log_prob_exact_fixed():
     assert np.abs(dl.cpu().numpy() - dl_ref).max() <= 2e-3
     lp = h.base_log_prob(x) + dl
     assert np.abs(lp.cpu().numpy() - lp_ref).max() <= 2e-3
+
+
+@pytest.mark.parametrize("name,B,dt", [("lj13", 3, 1.0), ("aldp", 2, 1.0), ("lj13", 3, 0.05), ("aldp", 2, 0.1)])
+def test_log_prob_exact_sparse_block1(name, B, dt):
+    """Exact trace where block 1 runs every edge as a primal tile and only the 2(N-1) edges at the unit tangent's
+    atom as dual tiles (egnn_eval sparse_a; LJ13: 5 primal + 1 dual tile per molecule, ALDP 15 + 2): vs the all-dual
+    form of the same kernel (ECNF_EXACT_SPARSE=0) and vs the fp64 oracle's full N*D trace."""
+    cfg = CONFIGS[name]
+    oc, params, h, z, x0, feat = setup(cfg, B=B)
+    opts = SolveOptions("euler", dt)
+    x, dl, _, st = h.integrate(g(x0), g(feat, torch.int32), 1.0, 0.0, opts, divergence=_lib.DIV_EXACT)
+    os.environ["ECNF_EXACT_SPARSE"] = "0"
+    try:
+        xd, dld, _, std = h.integrate(g(x0), g(feat, torch.int32), 1.0, 0.0, opts, divergence=_lib.DIV_EXACT)
+    finally:
+        del os.environ["ECNF_EXACT_SPARSE"]
+    assert (st.cpu().numpy() == 0).all() and (std.cpu().numpy() == 0).all()
+    _, _, dl_ref, _, x_ref = O.get_log_prob(params, oc, x0, feat, approx=False, solver="euler", dt0=dt,
+                                            dtype=np.float64)
+    # the skipped edge tangents are exact zeros: the two forms differ only by rounding (receiver a's segment sum
+    # runs over different lanes; the primal tiles take the primal kernels' code path)
+    ex, edl = float((x - xd).abs().max()), float((dl - dld).abs().max())
+    ox, odl = np.abs(x.cpu().numpy() - x_ref).max(), np.abs(dl.cpu().numpy() - dl_ref).max()
+    oxd, odld = np.abs(xd.cpu().numpy() - x_ref).max(), np.abs(dld.cpu().numpy() - dl_ref).max()
+    print(f"{name} dt={dt}: sparse vs dense |dx| {ex:.3g} |ddl| {edl:.3g}; vs fp64: sparse |dx| {ox:.3g} |ddl| "
+          f"{odl:.3g}, dense |dx| {oxd:.3g} |ddl| {odld:.3g}")
+    assert ox <= 1e-4 and odl <= 2e-3, (ox, odl)
+    assert ex <= 1e-5 and edl <= 1e-4 * max(1.0, float(dld.abs().max())), (ex, edl)
 
 
 def test_sample_and_log_prob_hutchinson_fixed():
