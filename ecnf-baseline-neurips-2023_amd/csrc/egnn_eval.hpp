@@ -1070,12 +1070,14 @@ __device__ __forceinline__ void edge_layer1_dual(const Net& net, const BlockW& b
 }
 
 // one 32-edge tile through phi_e / gate / phi_x  (egnn.py:72-95)
-// a >= 0 (split tangent kernels only, exact trace, block 1): `tile` is a molecule and the tile is dual tile `part`
-// of the 2(N - 1) edges at atom a of that molecule, in receiver-major order (receivers i < a with sender a, then
-// receiver a with its N - 1 senders in graph.py order, then receivers i > a), storing tangent outputs only
+// a >= 0 (split tangent kernels only, exact trace, egnn_eval sparse_a): `tile` is a molecule and the tile is dual
+// tile `part` of 2(N - 1) edges of that molecule, in receiver-major order, storing tangent outputs only.
+//   amode 1 (block 1): the edges at atom a (receivers i < a with sender a, receiver a with its N - 1 senders in
+//                      graph.py order, receivers i > a with sender a)
+//   amode 2 (last block): the edges INTO atoms 0 and a (receiver 0's N - 1 edges, then receiver a's; a >= 1)
 template <int NF, int NT, int L, int D, int P>
 __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, const Lds& s, int tile, int lane, bool agg,
-                                          int a = -1, int part = 0) {
+                                          int a = -1, int part = 0, int amode = 1) {
   const int kk = lane >> 5, li = lane & 31;
 #ifdef ECNF_EXP_CHAIN_ONLY
   {  // timing experiment: the two chain segments alone, on synthetic activations, one LDS add as the sink
@@ -1114,7 +1116,11 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
     mol = tile;
     const int q = part * 32 + li;
     valid = q < 2 * nn1;
-    if (q < a) {
+    if (amode == 2) {   // receiver 0 (senders 1 .. N - 1), then receiver a (senders (a + 1 + j) mod N)
+      i = q < nn1 ? 0 : a;
+      sd = q < nn1 ? q + 1 : a + 1 + (q - nn1);
+      if (sd >= N) sd -= N;
+    } else if (q < a) {
       i = q;
       sd = a;
     } else if (q < a + nn1) {   // receiver a, sender (a + 1 + j) mod N with j = q - a
@@ -1491,21 +1497,25 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
         for (int i = 0; i < q; ++i) mm &= mm - 1u;   // drop the q lowest active molecules
         return __builtin_ctz(mm);
       };
-      // exact trace, block 1 (sparse_a = the unit tangent's atom): h carries no tangent yet (embedding and time
-      // only), so an edge's tangent is nonzero only if it touches atom a (dr = 0 otherwise, and the chains, gate
-      // and shift of a zero input tangent are exactly zero).  Every edge runs as a primal tile and the 2(N - 1)
-      // edges at a as dual tiles storing tangents only: per molecule tpm primal + ceil(2(N - 1) / 32) dual tiles
-      // instead of tpm dual tiles (the dual tiles are dealt first)
+      // exact trace (sparse_a = the unit tangent's atom; joint_field): two blocks need only 2(N - 1) edge tangents.
+      //  * block 1: h carries no tangent yet (embedding and time only), so an edge's tangent is nonzero only if it
+      //    touches atom a (dr = 0 otherwise, and the chains, gate and shift of a zero input tangent are exactly 0);
+      //  * the last block (K > 1): it updates x only, and the trace reads the JVP at atoms a and 0 only
+      //    (joint_field: tout[k] - tout[k mod D]), so only the edges into those two atoms need tangents (the other
+      //    atoms' tangent rows go stale; nothing reads them).
+      // There every edge runs as a primal tile and the 2(N - 1) edges as dual tiles storing tangents only: per
+      // molecule tpm primal + ceil(2(N - 1) / 32) dual tiles instead of tpm dual tiles (dual tiles dealt first)
       int ndt = 0;
+      const int amode = k == 0 ? 1 : 2;
       if constexpr (Geo<NF, NT, P>::kL2T)
-        if (sparse_a >= 0 && k == 0) ndt = (2 * (N - 1) + 31) >> 5;
+        if (sparse_a >= 0 && (k == 0 || k + 1 == net.K)) ndt = (2 * (N - 1) + 31) >> 5;
       const int nd = nact * ndt;
       const int nrun = nd + nact * tpm;
       for (int vt = wave; vt < nrun; vt += kNW) {
         if constexpr (Geo<NF, NT, P>::kL2T) {
           if (vt < nd) {
             const int q = vt / ndt;
-            edge_tile<NF, NT, L, D, P>(net, bw, s, nth_active(q), elane, need_h, sparse_a, vt - q * ndt);
+            edge_tile<NF, NT, L, D, P>(net, bw, s, nth_active(q), elane, need_h, sparse_a, vt - q * ndt, amode);
             continue;
           }
         }

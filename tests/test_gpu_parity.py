@@ -236,8 +236,9 @@ def test_log_prob_exact_fixed():
 
 @pytest.mark.parametrize("name,B,dt", [("lj13", 3, 1.0), ("aldp", 2, 1.0), ("lj13", 3, 0.05), ("aldp", 2, 0.1)])
 def test_log_prob_exact_sparse_block1(name, B, dt):
-    """Exact trace where block 1 runs every edge as a primal tile and only the 2(N-1) edges at the unit tangent's
-    atom as dual tiles (egnn_eval sparse_a; LJ13: 5 primal + 1 dual tile per molecule, ALDP 15 + 2): vs the all-dual
+    """Exact trace where blocks 1 and K run every edge as a primal tile and only 2(N-1) edges as dual tiles
+    (egnn_eval sparse_a; block 1: the edges at the unit tangent's atom a, block K: the edges into atoms 0 and a, the
+    two JVP components the trace reads; LJ13: 5 primal + 1 dual tile per molecule, ALDP 15 + 2): vs the all-dual
     form of the same kernel (ECNF_EXACT_SPARSE=0) and vs the fp64 oracle's full N*D trace."""
     cfg = CONFIGS[name]
     oc, params, h, z, x0, feat = setup(cfg, B=B)
