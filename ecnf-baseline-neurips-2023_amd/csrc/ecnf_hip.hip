@@ -245,6 +245,8 @@ struct ecnf_handle {
   Net net[4];          // [2 P + NT], at the LDS-optimal molecules per workgroup (choose_mpw)
   size_t lds[4];       // dynamic LDS bytes per workgroup [2 P + NT]
   int ncu;             // compute units of the device (batch-aware workgroup sizing, net_for_batch)
+  float* pcache;       // exact trace: primal-aggregate cache of the sparse blocks (SolveP::pcache), grown on demand
+  size_t pcache_floats;
 };
 
 namespace {
@@ -852,6 +854,7 @@ int ecnf_destroy(ecnf_handle* h) {
   HIP_TRY(hipSetDevice(h->device));
   HIP_TRY(hipDeviceSynchronize());
   HIP_TRY(hipFree(h->dbuf));
+  if (h->pcache) HIP_TRY(hipFree(h->pcache));
   delete h;
   return ECNF_OK;
 }
@@ -955,6 +958,25 @@ int ecnf_integrate(ecnf_handle* h, const ecnf_solve_opts* o, const float* y0, co
     sp.sparse1 = (o->divergence == ECNF_DIV_EXACT && tpm >= 3 * ndt && !(env && std::atoi(env) == 0)) ? 1 : 0;
   }
   HIP_TRY(hipSetDevice(h->device));
+  // the primal-aggregate cache of the sparse blocks (one slot per molecule of the grid: <= batch + MPW - 1);
+  // ECNF_EXACT_PCACHE=0 turns it off (every JVP pass then recomputes the primal tiles)
+  sp.pcache = nullptr;
+  if (sp.sparse1) {
+    const char* env = std::getenv("ECNF_EXACT_PCACHE");
+    if (!(env && std::atoi(env) == 0)) {
+      const ecnf_cfg& c = h->cfg;
+      const size_t need = (size_t)(batch + h->net[2 * h->prec + 1].MPW) *
+                          ((size_t)c.n_nodes * c.mlp_width + 2 * (size_t)c.n_nodes * c.dim);
+      if (h->pcache_floats < need) {
+        if (h->pcache) HIP_TRY(hipFree(h->pcache));
+        h->pcache = nullptr;
+        h->pcache_floats = 0;
+        HIP_TRY(hipMalloc(&h->pcache, need * sizeof(float)));
+        h->pcache_floats = need;
+      }
+      sp.pcache = h->pcache;
+    }
+  }
   HIP_TRY(dispatch_integrate(h, NT, sp, y0, feat, eps, y1, dlogp, nfe, status, batch, (hipStream_t)stream));
   g_err.clear();
   return ECNF_OK;

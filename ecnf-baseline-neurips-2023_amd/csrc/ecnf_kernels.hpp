@@ -43,6 +43,10 @@ struct SolveP {
   // (egnn_eval sparse_a; set by the host where it pays: the M <= 128 split tangent kernels, >= 3 tiles per molecule
   // per dual tile)
   int sparse1;
+  // exact trace with sparse1: per-molecule cache of the primal edge aggregates of blocks 1 and K ([molecule slot of
+  // the grid][N M + 2 N D] floats), written by the first JVP pass of an evaluation and read by the other ND - D - 1
+  // (the primal is the same in every pass), which then run only the dual tiles of those blocks.  nullptr: off
+  float* pcache;
 };
 
 // solver state in LDS, after the eval region
@@ -115,8 +119,12 @@ __device__ __forceinline__ void joint_field(const Net& net, const Lds& s, const 
     }
     // exact: the unit tangent e_k sits on atom k / D, so block 1 (whose node features carry no tangent) has nonzero
     // edge tangents only on the 2(N - 1) edges at that atom
-    egnn_eval<NF, NT, L, D, P>(net, s, st.ys, st.ts, st.tin, st.vout, st.tout, st.active,
-                               exact && sp.sparse1 ? k / D : -1);
+    const bool sparse = exact && sp.sparse1;
+    float* pc = sparse && sp.pcache
+                    ? sp.pcache + (size_t)blockIdx.x * MPW * (net.N * (NF * 32) + 2 * net.N * D)
+                    : nullptr;
+    egnn_eval<NF, NT, L, D, P>(net, s, st.ys, st.ts, st.tin, st.vout, st.tout, st.active, sparse ? k / D : -1, pc,
+                               k0 == 0 ? 1 : 2);
     if constexpr (NT) {
       if (tid < MPW) {
         if (sp.div == ECNF_DIV_HUTCHINSON) {

@@ -1380,7 +1380,8 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
 // ---------------------------------------------------------------------------------------------------
 template <int NF, int NT, int L, int D, int P>
 __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const float* x_in, const float* t_in, const float* tan_in,
-                          float* v_out, float* tan_out, const int* act = nullptr, int sparse_a = -1) {
+                          float* v_out, float* tan_out, const int* act = nullptr, int sparse_a = -1,
+                          float* pcache = nullptr, int pmode = 0) {
   constexpr int kNW = Geo<NF, NT, P>::NW, kNT = Geo<NF, NT, P>::NTHR;
   constexpr bool kSplitG = Geo<NF, NT, P>::kSplit;
   constexpr bool kSplitN = Geo<NF, NT, P>::kSplitN;   // split node GEMMs (primal split kernels and tangent kernels)
@@ -1509,8 +1510,24 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
       const int amode = k == 0 ? 1 : 2;
       if constexpr (Geo<NF, NT, P>::kL2T)
         if (sparse_a >= 0 && (k == 0 || k + 1 == net.K)) ndt = (2 * (N - 1) + 31) >> 5;
+      // primal aggregates of the sparse blocks cached over the JVP passes of one evaluation (pcache, joint_field):
+      // pass 1 stores them after the edge phase (pmode 1), later passes load them here and run only the dual tiles
+      // (pmode 2).  Dual tiles store tangent rows only, so the loaded primal rows are not raced.
+      const int pstride = N * M + 2 * N * D;
+      const bool pload = ndt && pcache && pmode == 2;
+      if (pload) {
+        for (int idx = tid; idx < MPW * N * M; idx += kNT) {
+          const int r = idx / M, c = idx - r * M, m = r / N;
+          if ((amask >> m) & 1u && k == 0) s.macc[r * s.ld_m + c] = pcache[m * pstride + (r - m * N) * M + c];
+        }
+        for (int idx = tid; idx < MPW * N * D; idx += kNT) {
+          const int r = idx / D, m = r / N;
+          if ((amask >> m) & 1u)
+            s.dxacc[idx] = pcache[m * pstride + N * M + (k == 0 ? 0 : N * D) + (idx - m * N * D)];
+        }
+      }
       const int nd = nact * ndt;
-      const int nrun = nd + nact * tpm;
+      const int nrun = nd + (pload ? 0 : nact * tpm);
       for (int vt = wave; vt < nrun; vt += kNW) {
         if constexpr (Geo<NF, NT, P>::kL2T) {
           if (vt < nd) {
@@ -1532,6 +1549,22 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
     }
 #endif
     __syncthreads();
+    if constexpr (Geo<NF, NT, P>::kL2T) {
+      // first JVP pass of an exact-trace evaluation: cache the sparse block's primal aggregates (see the edge loop)
+      if (pcache && pmode == 1 && sparse_a >= 0 && (k == 0 || k + 1 == net.K)) {
+        const int pstride = N * M + 2 * N * D;
+        if (k == 0)
+          for (int idx = tid; idx < MPW * N * M; idx += kNT) {
+            const int r = idx / M, c = idx - r * M, m = r / N;
+            pcache[m * pstride + (r - m * N) * M + c] = s.macc[r * s.ld_m + c];
+          }
+        for (int idx = tid; idx < MPW * N * D; idx += kNT) {
+          const int m = idx / (N * D);
+          pcache[m * pstride + N * M + (k == 0 ? 0 : N * D) + (idx - m * N * D)] = s.dxacc[idx];
+        }
+        __syncthreads();
+      }
+    }
     STAMP(s, kStEdge);
     tid = opaque_tid();
     lane = tid & 63;

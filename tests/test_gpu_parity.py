@@ -234,33 +234,46 @@ def test_log_prob_exact_fixed():
     assert np.abs(lp.cpu().numpy() - lp_ref).max() <= 2e-3
 
 
+def _exact_env(sparse, pcache):
+    os.environ["ECNF_EXACT_SPARSE"] = sparse
+    os.environ["ECNF_EXACT_PCACHE"] = pcache
+
+
 @pytest.mark.parametrize("name,B,dt", [("lj13", 3, 1.0), ("aldp", 2, 1.0), ("lj13", 3, 0.05), ("aldp", 2, 0.1)])
 def test_log_prob_exact_sparse_block1(name, B, dt):
     """Exact trace where blocks 1 and K run every edge as a primal tile and only 2(N-1) edges as dual tiles
     (egnn_eval sparse_a; block 1: the edges at the unit tangent's atom a, block K: the edges into atoms 0 and a, the
-    two JVP components the trace reads; LJ13: 5 primal + 1 dual tile per molecule, ALDP 15 + 2): vs the all-dual
-    form of the same kernel (ECNF_EXACT_SPARSE=0) and vs the fp64 oracle's full N*D trace."""
+    two JVP components the trace reads; LJ13: 5 primal + 1 dual tile per molecule, ALDP 15 + 2), and where the
+    primal aggregates of those blocks are cached over the ND - D JVP passes of an evaluation (SolveP::pcache): vs
+    the all-dual form of the same kernel (ECNF_EXACT_SPARSE=0), the sparse form without the cache
+    (ECNF_EXACT_PCACHE=0), and the fp64 oracle's full N*D trace."""
     cfg = CONFIGS[name]
     oc, params, h, z, x0, feat = setup(cfg, B=B)
     opts = SolveOptions("euler", dt)
-    x, dl, _, st = h.integrate(g(x0), g(feat, torch.int32), 1.0, 0.0, opts, divergence=_lib.DIV_EXACT)
-    os.environ["ECNF_EXACT_SPARSE"] = "0"
+    out = {}
     try:
-        xd, dld, _, std = h.integrate(g(x0), g(feat, torch.int32), 1.0, 0.0, opts, divergence=_lib.DIV_EXACT)
+        for form, env in (("dense", ("0", "1")), ("sparse", ("1", "0")), ("cached", ("1", "1"))):
+            _exact_env(*env)
+            x, dl, _, st = h.integrate(g(x0), g(feat, torch.int32), 1.0, 0.0, opts, divergence=_lib.DIV_EXACT)
+            assert (st.cpu().numpy() == 0).all()
+            out[form] = (x, dl)
     finally:
-        del os.environ["ECNF_EXACT_SPARSE"]
-    assert (st.cpu().numpy() == 0).all() and (std.cpu().numpy() == 0).all()
+        del os.environ["ECNF_EXACT_SPARSE"], os.environ["ECNF_EXACT_PCACHE"]
     _, _, dl_ref, _, x_ref = O.get_log_prob(params, oc, x0, feat, approx=False, solver="euler", dt0=dt,
                                             dtype=np.float64)
-    # the skipped edge tangents are exact zeros: the two forms differ only by rounding (receiver a's segment sum
-    # runs over different lanes; the primal tiles take the primal kernels' code path)
-    ex, edl = float((x - xd).abs().max()), float((dl - dld).abs().max())
+    x, dl = out["cached"]
     ox, odl = np.abs(x.cpu().numpy() - x_ref).max(), np.abs(dl.cpu().numpy() - dl_ref).max()
-    oxd, odld = np.abs(xd.cpu().numpy() - x_ref).max(), np.abs(dld.cpu().numpy() - dl_ref).max()
-    print(f"{name} dt={dt}: sparse vs dense |dx| {ex:.3g} |ddl| {edl:.3g}; vs fp64: sparse |dx| {ox:.3g} |ddl| "
-          f"{odl:.3g}, dense |dx| {oxd:.3g} |ddl| {odld:.3g}")
+    print(f"{name} dt={dt}: vs fp64 |dx| {ox:.3g} |ddl| {odl:.3g}")
     assert ox <= 1e-4 and odl <= 2e-3, (ox, odl)
-    assert ex <= 1e-5 and edl <= 1e-4 * max(1.0, float(dld.abs().max())), (ex, edl)
+    # the skipped edge tangents are exact zeros and the cached aggregates are the recomputed ones: the forms differ
+    # at most by rounding (receiver a's block-1 segment sum runs over different lanes)
+    xd, dld = out["dense"]
+    for form in ("sparse", "cached"):
+        xf, dlf = out[form]
+        ex, edl = float((xf - xd).abs().max()), float((dlf - dld).abs().max())
+        print(f"{name} dt={dt}: {form} vs dense |dx| {ex:.3g} |ddl| {edl:.3g}")
+        assert ex <= 1e-5 and edl <= 1e-4 * max(1.0, float(dld.abs().max())), (form, ex, edl)
+    assert torch.equal(out["sparse"][0], out["cached"][0]) and torch.equal(out["sparse"][1], out["cached"][1])
 
 
 def test_sample_and_log_prob_hutchinson_fixed():

@@ -1,5 +1,5 @@
 """Diagnostic for the exact trace's sparse dual tiles (blocks 1 and K): ECNF_EXACT_SPARSE=0 (every tile dual) vs the
-default; LJ13, B = 3, one Euler step of dt = 1 (one evaluation) and 20 steps of 0.05."""
+default (1 = sparse without, 2 = with the primal-aggregate cache); LJ13, B = 3, one Euler step of dt = 1 (one evaluation) and 20 steps of 0.05."""
 import os
 import sys
 
@@ -22,10 +22,13 @@ feat = np.zeros((3, cfg.n_nodes), np.int32)
 g = lambda a, t=torch.float32: torch.as_tensor(a, device="cuda", dtype=t)
 for dt in (1.0, 0.05):
     res = {}
-    for mode in (0, 1):
-        os.environ["ECNF_EXACT_SPARSE"] = str(mode)
+    for mode, (sparse, pcache) in enumerate([("0", "1"), ("1", "0"), ("1", "1")]):
+        os.environ["ECNF_EXACT_SPARSE"] = sparse
+        os.environ["ECNF_EXACT_PCACHE"] = pcache
         x, dl, _, st = h.integrate(g(x0), g(feat, torch.int32), 1.0, 0.0, SolveOptions("euler", dt),
                                    divergence=_lib.DIV_EXACT)
         res[mode] = (x.cpu().numpy(), dl.cpu().numpy())
-    print(f"dt {dt}: |x - x_dense| {np.abs(res[1][0] - res[0][0]).max():.3g}  "
-          f"|dl - dl_dense| {np.abs(res[1][1] - res[0][1]).max():.3g} (|dl| {np.abs(res[0][1]).max():.3g})", flush=True)
+    for mode in (1, 2):
+        print(f"dt {dt} form {mode}: |x - x_dense| {np.abs(res[mode][0] - res[0][0]).max():.3g}  "
+              f"|dl - dl_dense| {np.abs(res[mode][1] - res[0][1]).max():.3g} (|dl| {np.abs(res[0][1]).max():.3g})",
+              flush=True)
