@@ -1385,6 +1385,11 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
   constexpr int kNW = Geo<NF, NT, P>::NW, kNT = Geo<NF, NT, P>::NTHR;
   constexpr bool kSplitG = Geo<NF, NT, P>::kSplit;
   constexpr bool kSplitN = Geo<NF, NT, P>::kSplitN;   // split node GEMMs (primal split kernels and tangent kernels)
+  // the exact trace's sparse blocks (primal + dual tiles, see the edge loop) in the M <= 128 split tangent kernels;
+  // not compiled for the L = 2 shapes (M, D) = (128, 3), (64, 2), where the primal tile's code beside the dual
+  // tile's spilled 36 B per lane (tests/test_kernel_resources.py).  The BASELINE shapes (LJ13 128/3/3, ALDP 64/2/3,
+  // DW4 128/3/2) have it.
+  constexpr bool kSparseX = Geo<NF, NT, P>::kL2T && !(L == 2 && (NF == 4 || D == 2));
   const int tid = opaque_tid(), lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: task indices stay in SGPRs
   const int N = net.N, H = net.H, T = net.T, M = NF * 32, RP = net.RP, MPW = net.MPW, ND = net.ND;
@@ -1508,7 +1513,7 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
       // molecule tpm primal + ceil(2(N - 1) / 32) dual tiles instead of tpm dual tiles (dual tiles dealt first)
       int ndt = 0;
       const int amode = k == 0 ? 1 : 2;
-      if constexpr (Geo<NF, NT, P>::kL2T)
+      if constexpr (kSparseX)
         if (sparse_a >= 0 && (k == 0 || k + 1 == net.K)) ndt = (2 * (N - 1) + 31) >> 5;
       // primal aggregates of the sparse blocks cached over the JVP passes of one evaluation (pcache, joint_field):
       // pass 1 stores them after the edge phase (pmode 1), later passes load them here and run only the dual tiles
@@ -1529,7 +1534,7 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
       const int nd = nact * ndt;
       const int nrun = nd + (pload ? 0 : nact * tpm);
       for (int vt = wave; vt < nrun; vt += kNW) {
-        if constexpr (Geo<NF, NT, P>::kL2T) {
+        if constexpr (kSparseX) {
           if (vt < nd) {
             const int q = vt / ndt;
             edge_tile<NF, NT, L, D, P>(net, bw, s, nth_active(q), elane, need_h, sparse_a, vt - q * ndt, amode);
@@ -1538,7 +1543,7 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
         }
         const int v2 = vt - nd, q = v2 / tpm;
         const int tile = nth_active(q) * tpm + (v2 - q * tpm);
-        if constexpr (Geo<NF, NT, P>::kL2T) {
+        if constexpr (kSparseX) {
           if (ndt) {
             edge_tile<NF, 0, L, D, P>(net, bw, s, tile, elane, need_h);
             continue;
@@ -1549,7 +1554,7 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
     }
 #endif
     __syncthreads();
-    if constexpr (Geo<NF, NT, P>::kL2T) {
+    if constexpr (kSparseX) {
       // first JVP pass of an exact-trace evaluation: cache the sparse block's primal aggregates (see the edge loop)
       if (pcache && pmode == 1 && sparse_a >= 0 && (k == 0 || k + 1 == net.K)) {
         const int pstride = N * M + 2 * N * D;
