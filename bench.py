@@ -85,66 +85,93 @@ def roofline_peak(cfg, chain_mode: str) -> float:
     return F / ((F - Fv) / p_split + Fv / PEAK_FP32_MFMA_TFLOPS)
 
 
-class ClockSampler:
-    """Samples the shader clock (the current level of the device's sysfs pp_dpm_sclk) and the board power (hwmon) of
-    OUR device (matched by PCI address) on a host thread while the timed region runs.  The split-fp16 MFMA-dense
-    kernel does not hold 2.4 GHz, so the roofline also reports the fraction at the sampled clock.
-    Returns None fields when sysfs is not readable."""
+PMC_PASSES = (("FETCH_SIZE", "GRBM_GUI_ACTIVE", "SQ_VALU_MFMA_BUSY_CYCLES", "SQ_BUSY_CYCLES"), ("WRITE_SIZE",))
+N_XCD, N_SIMD = 8, 1024
 
-    def __init__(self, dev):
-        import glob
-        import threading
-        self.card = None
-        try:
-            import torch
-            p = torch.cuda.get_device_properties(dev)
-            bus = f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}"
-            for c in glob.glob("/sys/class/drm/card*/device"):
-                if os.path.basename(os.path.realpath(c)).startswith(bus):
-                    self.card = c
-                    break
-        except Exception:
-            self.card = None
-        self.sclk, self.power = [], []
-        self._stop = threading.Event()
-        self._t = threading.Thread(target=self._run, daemon=True)
 
-    def _read(self):
-        with open(os.path.join(self.card, "pp_dpm_sclk")) as f:
-            for line in f:
-                if line.rstrip().endswith("*"):
-                    self.sclk.append(float(line.split(":")[1].strip().rstrip("*").strip().lower().rstrip("mhz")))
-        import glob
-        for pf in glob.glob(os.path.join(self.card, "hwmon", "hwmon*", "power1_*")):
-            if pf.endswith(("power1_average", "power1_input")):
-                with open(pf) as f:
-                    self.power.append(float(f.read()) / 1e6)
-                break
+def _read_counters(d):
+    """{dispatch id: {counter: value summed over its instances}} from a rocprofv3 --pmc CSV under directory d."""
+    import csv
+    import glob
+    out = {}
+    for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(path)):
+            dd = out.setdefault(int(r["Dispatch_Id"]), {})
+            dd[r["Counter_Name"]] = dd.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+    return out
 
-    def _run(self):
-        while not self._stop.is_set():
+
+def _read_durations(d):
+    """{dispatch id: kernel duration in ns} from the rocprofv3 kernel trace under directory d."""
+    import csv
+    import glob
+    out = {}
+    for path in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
+        for r in csv.DictReader(open(path)):
+            out[int(r["Dispatch_Id"])] = float(r["End_Timestamp"]) - float(r["Start_Timestamp"])
+    return out
+
+
+def collect_pmc(child_args, timeout_s=150):
+    """HBM traffic, effective clock and MFMA-pipe occupancy of the dominant kernel, measured in this bench run: the
+    same workload is launched by a child `bench.py --pmc-child` under rocprofv3, one counter pass per group of
+    PMC_PASSES (FETCH_SIZE and WRITE_SIZE cannot share a pass: 3 + 2 TCC counters), with the kernel trace for the
+    per-dispatch duration.  Corrections per MI355X_MICROARCH.md (HBM / rocprofv3): FETCH_SIZE reports half of the
+    bytes of 16-B-per-lane reads on gfx950 (every weight load here is a 16-B buffer_load), so HBM bytes =
+    2 x FETCH_SIZE + WRITE_SIZE (KiB); effective clock = GRBM_GUI_ACTIVE / 8 XCDs / duration; MFMA pipe busy =
+    SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs).  Returns None when rocprofv3 is unavailable or a
+    pass fails (the bench line then reports traffic null)."""
+    import shutil
+    import signal
+    import statistics
+    import tempfile
+    prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(prof):
+        return None
+    vals, durs = {}, {}
+    with tempfile.TemporaryDirectory(prefix="ecnf_pmc_", dir=os.environ.get("TMPDIR", "/tmp")) as tmp:
+        for k, counters in enumerate(PMC_PASSES):
+            d = os.path.join(tmp, f"p{k}")
+            cmd = [prof, "--pmc", *counters, "--kernel-trace", "--kernel-include-regex", "integrate_kernel",
+                   "-d", d, "-o", "run", "--output-format", "csv", "--",
+                   sys.executable, os.path.abspath(__file__), "--pmc-child", *child_args]
+            env = dict(os.environ, TMPDIR=tmp)
+            p = subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, env=env, start_new_session=True)
             try:
-                self._read()
-            except Exception:
-                return
-            time.sleep(0.002)
-
-    def __enter__(self):
-        if self.card:
-            self._t.start()
-        return self
-
-    def __exit__(self, *exc):
-        self._stop.set()
-        if self.card:
-            self._t.join(timeout=1.0)
-
-    def summary(self):
-        import statistics
-        return {"sclk_mhz_median": statistics.median(self.sclk) if self.sclk else None,
-                "power_w_median": statistics.median(self.power) if self.power else None,
-                "samples": len(self.sclk),
-                "source": "sysfs pp_dpm_sclk / hwmon of the device's PCI address, sampled every 2 ms in the timed region"}
+                _, err = p.communicate(timeout=timeout_s)
+            except subprocess.TimeoutExpired:
+                os.killpg(p.pid, signal.SIGKILL)
+                p.wait()
+                print(f"[bench] PMC pass {counters} timed out", file=sys.stderr, flush=True)
+                return None
+            if p.returncode != 0:
+                print(f"[bench] PMC pass {counters} failed: {err.decode(errors='replace')[-800:]}", file=sys.stderr,
+                      flush=True)
+                return None
+            for disp, cv in _read_counters(d).items():
+                vals.setdefault(k, {})[disp] = cv
+            if k == 0:
+                durs = _read_durations(d)
+    try:
+        # the child runs one warm-up launch and then the measured ones: drop each pass's first dispatch
+        def per_launch(k, name):
+            ds = sorted(vals[k])[1:] or sorted(vals[k])
+            return statistics.median(vals[k][x][name] for x in ds), ds
+        fetch_kib, ds0 = per_launch(0, "FETCH_SIZE")
+        write_kib, _ = per_launch(1, "WRITE_SIZE")
+        gui, _ = per_launch(0, "GRBM_GUI_ACTIVE")
+        busy, _ = per_launch(0, "SQ_VALU_MFMA_BUSY_CYCLES")
+        dur_ns = statistics.median(durs[x] for x in ds0 if x in durs) if durs else None
+    except (KeyError, ValueError, statistics.StatisticsError):
+        return None
+    clock = gui / N_XCD / (dur_ns * 1e-9) / 1e9 if dur_ns else None
+    return {"hbm_bytes_per_launch": (2.0 * fetch_kib + write_kib) * 1024.0,
+            "fetch_bytes_per_launch": 2.0 * fetch_kib * 1024.0, "write_bytes_per_launch": write_kib * 1024.0,
+            "fetch_size_kib_raw": fetch_kib, "grbm_gui_active": gui, "sq_valu_mfma_busy_cycles": busy,
+            "kernel_ms_in_pmc_run": dur_ns * 1e-6 if dur_ns else None, "clock_ghz_grbm": clock,
+            "mfma_pipe_busy_frac": busy / (gui / N_XCD * N_SIMD) if gui else None,
+            "source": "rocprofv3 --pmc (2 passes) + --kernel-trace of a child bench.py --pmc-child on the same "
+                      "workload, inside this bench run; FETCH_SIZE doubled per the gfx950 16-B/lane correction"}
 
 
 def cpu_model() -> str:
@@ -224,6 +251,10 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL over xGMI) or gloo (multi-rank rehearsal)")
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--dump", default="", help="directory: each rank saves its shard's outputs (tests)")
+    ap.add_argument("--pmc", type=int, default=-1,
+                    help="measure HBM traffic / clock / MFMA busy with rocprofv3 counter passes of this workload "
+                         "(default: on at one rank, off over several)")
+    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -232,7 +263,7 @@ def main():
     import numpy as np
     import torch
     import torch.distributed as dist
-    from ecnf_amd import CONFIGS, init_params
+    from ecnf_amd import CONFIGS, init_params, param_count
     from ecnf_amd import _lib
     from ecnf_amd import distributed as D
     from ecnf_amd.engine import EcnfHandle, SolveOptions
@@ -266,6 +297,13 @@ def main():
     def step():
         return h.integrate(x0, feat, 0.0, 1.0, opts, check_status=False)
 
+    if args.pmc_child:
+        # under rocprofv3 (collect_pmc): one warm-up launch, then the measured launches of the same workload
+        for _ in range(1 + max(1, args.steps)):
+            step()
+        torch.cuda.synchronize(dev)
+        return
+
     for _ in range(args.warmup):
         y1, _, nfe, _ = step()
     torch.cuda.synchronize(dev)
@@ -286,14 +324,13 @@ def main():
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     barrier()
     torch.cuda.synchronize(dev)
-    with ClockSampler(local) as clock:
-        t0 = time.perf_counter()
-        for i in range(args.steps):
-            ev[i][0].record(stream)
-            y1, _, nfe, status = step()
-            ev[i][1].record(stream)
-        torch.cuda.synchronize(dev)
-        t_run = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        y1, _, nfe, status = step()
+        ev[i][1].record(stream)
+    torch.cuda.synchronize(dev)
+    t_run = time.perf_counter() - t0
     barrier()
     t_max = max_over_ranks(t_run)
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev])) if args.steps else 0.0
@@ -301,6 +338,8 @@ def main():
 
     value = G * args.steps / t_max
     F = live_flops_per_eval(cfg)
+    # algorithmic HBM bytes of one launch: x0 in, x1 / nfe / status out (fp32 / int32), one read of the weight set
+    algo_bytes = B * (2 * cfg.event_dim * 4 + 8) + 4 * param_count(cfg)
     achieved = F * nfe_seen * B / (kernel_ms * 1e-3) / 1e12
     chain_mode = h.chain_arithmetic()
     peak = roofline_peak(cfg, chain_mode)
@@ -337,20 +376,22 @@ def main():
             log_p = T.lj_log_prob(x1, cfg.n_nodes, cfg.dim) if args.config == "lj13" else \
                 T.dw_log_prob(x1, cfg.n_nodes, cfg.dim)
             log_w = log_p - log_q
-            fwd, rev = D.ess_from_device(log_w)       # RCCL: one MAX + one SUM all-reduce
+            # reverse ESS of model samples (eval_batch_free_fn, setup_training.py:166-185); the forward ESS needs
+            # samples of the TARGET (evaluation.py:10-22, on the test set: ecnf_amd.evaluation), not model samples
+            _, rev = D.ess_from_device(log_w)         # RCCL: one MAX + one SUM all-reduce
             mean_lq = D.masked_mean(log_q)
             torch.cuda.synchronize(dev)
             barrier()
             t_lp = max_over_ranks(time.perf_counter() - t1)
         logprob = {"workload": f"{args.config} sample_and_log_prob_cnf (Hutchinson, Euler NFE={args.nfe}) + target "
                                f"log-density + ESS over {'RCCL' if args.dist_backend == 'nccl' else args.dist_backend}",
-                   "molecules_per_s": G / t_lp, "ms": t_lp * 1e3, "rev_ess": float(rev), "fwd_ess": float(fwd),
+                   "molecules_per_s": G / t_lp, "ms": t_lp * 1e3, "rev_ess": float(rev),
                    "mean_log_q": float(mean_lq), "status_ok": bool(int((st != 0).sum()) == 0)}
         if args.dump:
             os.makedirs(args.dump, exist_ok=True)
             np.savez(os.path.join(args.dump, f"rank{rank}.npz"), lo=lo, hi=hi, x1=y1.cpu().numpy(),
                      x1_lp=x1.cpu().numpy(), log_q=log_q.cpu().numpy(), log_w=log_w.cpu().numpy(),
-                     rev_ess=float(rev), fwd_ess=float(fwd), mean_log_q=float(mean_lq), world=world)
+                     rev_ess=float(rev), mean_log_q=float(mean_lq), world=world)
 
     # training leg (SURVEY 8f rank 3, lj13.yaml training: Adam, batch 64): one flow_matching_update_fn step =
     # loss + reverse-mode gradient + Adam, on the same device (N = 1 only)
@@ -380,6 +421,12 @@ def main():
                              f"batch {args.train_batch}, strict-fp32 MFMA GEMMs",
                  "ms_per_step": ms, "steps_per_s": 1e3 / ms, "molecules_per_s": args.train_batch * 1e3 / ms,
                  "loss": float(loss)}
+
+    # HBM traffic, effective clock and MFMA occupancy of this workload's kernel, from counter passes run now
+    pmc = None
+    if rank == 0 and (args.pmc > 0 or (args.pmc < 0 and world == 1)):
+        pmc = collect_pmc(["--config", args.config, "--batch", str(G), "--nfe", str(args.nfe), "--seed",
+                           str(args.seed), "--steps", "2"])
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_molecules > 0:
@@ -414,15 +461,18 @@ def main():
             "matmul": {"gemms": chain_mode, "tangent_kernels": h.chain_arithmetic(True) + " edge chains",
                        "accumulate": "f32", "strict_fp32": fp32},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
-                         "frac": achieved / peak, "traffic": None,
+                         "frac": achieved / peak,
+                         "traffic": pmc["hbm_bytes_per_launch"] if pmc else None,
+                         "traffic_unit": "HBM bytes per launch (rocprofv3 FETCH_SIZE / WRITE_SIZE, this run)",
+                         "algorithmic_bytes_per_launch": algo_bytes,
                          "kernel": "integrate_kernel", "kernel_ms": kernel_ms,
                          "flop_per_launch": F * nfe_seen * B,
                          "flop_basis": "live dense-contraction FLOPs per EGNN eval (SURVEY 8d F minus the last "
                                        "block's dead h update) x NFE x batch",
                          "frac_vs_fp32_mfma_peak": achieved / PEAK_FP32_MFMA_TFLOPS,
-                         "device_clock": clock.summary(),
-                         "frac_at_sampled_sclk": (achieved / (peak * clock.summary()["sclk_mhz_median"] / 2400.0)
-                                                  if clock.summary()["sclk_mhz_median"] else None),
+                         "pmc": pmc,
+                         "frac_at_grbm_clock": (achieved / (peak * pmc["clock_ghz_grbm"] / 2.4)
+                                                if pmc and pmc.get("clock_ghz_grbm") else None),
                          "peak_basis": (f"GEMM FLOPs at the dense 16-bit MFMA peak / {SPLIT_TERMS[chain_mode]} split "
                                         "terms, vector FLOPs at the fp32 peak") if chain_mode in SPLIT_TERMS
                                        else "fp32 MFMA peak"},
@@ -430,10 +480,6 @@ def main():
             "train": train,
             "cpu_baseline": cpu,
         }
-        pmc = os.path.join(ROOT, "profiles", f"pmc_traffic_{args.config}_b{B}.json")
-        if os.path.exists(pmc):
-            with open(pmc) as f:
-                out["roofline"]["traffic"] = json.load(f).get("hbm_bytes_per_launch")
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -253,12 +253,25 @@ __shared__ unsigned g_ring[2 * kRingIV * kPieces * 256];
 // through the same layers.  Each weight fragment feeds 2 kTerms MFMAs (primal and tangent interleaved); the
 // tangent of a layer is du = accT inv (no bias) and dy' = silu'(t) du = r (1 - ln2 u (1 - r)) du with the primal's
 // r = 1 / (1 + 2^u) (silu'(t) = sigma(t) (1 + t (1 - sigma(t))), t = -ln2 u).
-template <int NF, int NL, int NT = 0>
+// WP: weight pieces per fragment group.  kPieces (2): the primal kernels' unscaled pieces, accumulators started at
+// the bias column (ECNF_CHAIN_BIAS_INIT).  3 (the divergence kernels, kWExact): the weights scaled by a power of two
+// per layer and split into three fp16 pieces w0 + w1 + w2 that hold the fp32 weight EXACTLY, the primal MFMAs adding
+// the fourth term w2 x0 (smallest first) and the activation applying 1/s and the bias in an FMA.  Two pieces represent
+// a weight only to 2^-22 (and unscaled small weights far worse, in fp16 subnormals): a FIXED perturbation of the
+// network, which the exact trace sums coherently over its N*D diagonal entries (LJ13: +1.2e-6 relative in tr J, 8x the
+// fp32 rounding error; tools/diag/trace_precision.py).  The tangent MFMAs keep three terms on pieces 0 and 1.
+template <int NF, int NL, int NT = 0, int WP = kPieces>
 __device__ __forceinline__ void chain_split(SplitX<NF>& XA, SplitX<NF>& XB, f32x16 (&acc)[NF],
                                             const unsigned* __restrict__ Wpk, const float* __restrict__ bias,
                                             const ChainInv& inv, int lane, SplitX<NF>& XAT, SplitX<NF>& XBT,
                                             f32x16 (&accT)[NF]) {
   using Plan = SplitPlan<NF, NL>;
+  static_assert(WP == kPieces || (WP == 3 && kPieces == 2), "3-piece weights extend the fp16 split");
+#ifdef ECNF_CHAIN_BIAS_INIT
+  constexpr bool kBI = WP == kPieces;
+#else
+  constexpr bool kBI = false;
+#endif
   // the chain wave issues first on its SIMD while its partner wave is in VALU / LDS work (A/B: 26.14 -> 25.99 ms)
   __builtin_amdgcn_s_setprio(ECNF_CHAIN_PRIO);
   constexpr int GB = Plan::GB, GL = Plan::GL, G = Plan::G, NI = Plan::NI, PF = ECNF_SPLIT_PF;
@@ -268,8 +281,9 @@ __device__ __forceinline__ void chain_split(SplitX<NF>& XA, SplitX<NF>& XB, f32x
   const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned*>(Wpk), (short)0,
                                                                          0x7fffffff, 0x00020000);
   const int voff = lane * 16;
-  u32x4 wbuf[PF + 1][kPieces];
+  u32x4 wbuf[PF + 1][WP];
 #ifdef ECNF_SPLIT_RING
+  static_assert(WP == kPieces, "the ring experiment streams two pieces");
   static_assert(G % kRingIV == 0, "segment groups must fill whole ring intervals");
   const int rwave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), rnw = blockDim.x >> 6;
   constexpr int kIvPieces = kRingIV * kPieces;
@@ -304,13 +318,12 @@ __device__ __forceinline__ void chain_split(SplitX<NF>& XA, SplitX<NF>& XB, f32x
 #pragma unroll
   for (int gg = 0; gg < PF && gg < G; ++gg)
 #pragma unroll
-    for (int p = 0; p < kPieces; ++p) wbuf[gg][p] = wload(rsrc, voff, (gg * kPieces + p) * kPieceBytes);
+    for (int p = 0; p < WP; ++p) wbuf[gg][p] = wload(rsrc, voff, (gg * WP + p) * kPieceBytes);
 #endif
   // per-item pipeline registers (SSA after unrolling: only live items occupy registers)
   f32x2 bv[NI], uv[NI], ev[NI], dv[NI], e2v[NI];
-#ifdef ECNF_CHAIN_BIAS_INIT
-  // each output block's accumulator starts at its (log2-domain) bias column and the weights are unscaled, so stage
-  // A needs no FMA; a block's 16 biases (rows acc_row(r, kk)) are 4 x 16-B LDS reads, issued 2 groups ahead
+  // kBI: each output block's accumulator starts at its (log2-domain) bias column and the weights are unscaled, so
+  // stage A needs no FMA; a block's 16 biases (rows acc_row(r, kk)) are 4 x 16-B LDS reads, issued 2 groups ahead
   auto bias_block = [&](int off) {
     f32x16 c;
     static_for<4>([&](auto Qc) {
@@ -323,26 +336,24 @@ __device__ __forceinline__ void chain_split(SplitX<NF>& XA, SplitX<NF>& XB, f32x
     });
     return c;
   };
-  f32x16 cb = bias_block(0);
-#else
-  static_for<Plan::count(0, 0)>([&](auto Kc) {
-    constexpr int id = Plan::nth(0, 0, decltype(Kc)::value);
-    bv[id] = *reinterpret_cast<const f32x2*>(lbias + Plan::bias_off(id));
-  });
-#endif
+  f32x16 cb = {};
+  if constexpr (kBI) {
+    cb = bias_block(0);
+  } else {
+    static_for<Plan::count(0, 0)>([&](auto Kc) {
+      constexpr int id = Plan::nth(0, 0, decltype(Kc)::value);
+      bv[id] = *reinterpret_cast<const f32x2*>(lbias + Plan::bias_off(id));
+    });
+  }
   static_for<GE>([&](auto GGc) {
     constexpr int gg = decltype(GGc)::value;
     constexpr bool mfma_group = gg < G;
     constexpr int l = gg / GL, g = gg % GL, jb = g / GB, fb = (g % GB) >> 1, u = g & 1;
     constexpr int nA = Plan::count(gg, 0), nB = Plan::count(gg, 1), nC = Plan::count(gg, 2);
-#ifdef ECNF_CHAIN_BIAS_INIT
-    constexpr int nbias = 0;
+    constexpr int nbias = kBI ? 0 : Plan::count(gg + 1, 0);
     constexpr int nxt = l * NF + jb + 1;   // the next output block of the segment
-    constexpr bool load_cb = mfma_group && (g % GB) == GB - 2 && nxt < NL * NF;
+    constexpr bool load_cb = kBI && mfma_group && (g % GB) == GB - 2 && nxt < NL * NF;
     if constexpr (load_cb) cb = bias_block((nxt / NF) * NF * 32 + (nxt % NF) * 32);
-#else
-    constexpr int nbias = Plan::count(gg + 1, 0);
-#endif
 #if defined(ECNF_SPLIT_RING)
     // next group's fragments from the ring, unless the next group opens a new interval (read after the barrier)
     if constexpr (gg + 1 < G && (gg + 1) % kRingIV != 0) ring_read(gg + 1, wbuf[(gg + 1) % (PF + 1)]);
@@ -356,8 +367,8 @@ __device__ __forceinline__ void chain_split(SplitX<NF>& XA, SplitX<NF>& XB, f32x
 #elif !defined(ECNF_SPLIT_NO_WLOAD)   // NO_WLOAD timing experiment: reuse the first PF groups' weights
     if constexpr (gg + PF < G) {
 #pragma unroll
-      for (int p = 0; p < kPieces; ++p)
-        wbuf[(gg + PF) % (PF + 1)][p] = wload(rsrc, voff, ((gg + PF) * kPieces + p) * kPieceBytes);
+      for (int p = 0; p < WP; ++p)
+        wbuf[(gg + PF) % (PF + 1)][p] = wload(rsrc, voff, ((gg + PF) * WP + p) * kPieceBytes);
     }
 #endif
     // biases of the next group's stage-A items
@@ -374,14 +385,15 @@ __device__ __forceinline__ void chain_split(SplitX<NF>& XA, SplitX<NF>& XB, f32x
       constexpr int pa = term_w(t), pb = term_x(t);   // cross terms, smallest first
       if constexpr (fb == 0 && u == 0 && t == 0) {
         const f32x16 z = {};
-#ifdef ECNF_CHAIN_BIAS_INIT
-        acc[jb] = mfma_split(A[pa], B[pb], cb);
-        if constexpr (NT) accT[jb] = mfma_split(A[pa], BT[pb], NT == 2 ? cb : z);
-#else
-        acc[jb] = mfma_split(A[pa], B[pb], z);
-        if constexpr (NT) accT[jb] = mfma_split(A[pa], BT[pb], z);
-#endif
+        if constexpr (WP == 3) {   // the exact-weight term w2 x0 first
+          acc[jb] = mfma_split(A[2], B[0], z);
+          acc[jb] = mfma_split(A[pa], B[pb], acc[jb]);
+        } else {
+          acc[jb] = mfma_split(A[pa], B[pb], kBI ? cb : z);
+        }
+        if constexpr (NT) accT[jb] = mfma_split(A[pa], BT[pb], (NT == 2 && kBI) ? cb : z);
       } else {
+        if constexpr (WP == 3 && t == 0) acc[jb] = mfma_split(A[2], B[0], acc[jb]);
         acc[jb] = mfma_split(A[pa], B[pb], acc[jb]);
         if constexpr (NT) accT[jb] = mfma_split(A[pa], BT[pb], accT[jb]);
       }
@@ -404,13 +416,13 @@ __device__ __forceinline__ void chain_split(SplitX<NF>& XA, SplitX<NF>& XB, f32x
       constexpr int id = Plan::nth(gg, 0, decltype(Kc)::value);
       constexpr typename Plan::Item it = Plan::item(id);
       constexpr int r = 2 * it.p;
-#ifdef ECNF_CHAIN_BIAS_INIT
-      uv[id][0] = acc[it.j][r];
-      uv[id][1] = acc[it.j][r + 1];
-#else
-      uv[id][0] = fmaf(acc[it.j][r], inv.v[it.l], bv[id][0]);
-      uv[id][1] = fmaf(acc[it.j][r + 1], inv.v[it.l], bv[id][1]);
-#endif
+      if constexpr (kBI) {
+        uv[id][0] = acc[it.j][r];
+        uv[id][1] = acc[it.j][r + 1];
+      } else {
+        uv[id][0] = fmaf(acc[it.j][r], inv.v[it.l], bv[id][0]);
+        uv[id][1] = fmaf(acc[it.j][r + 1], inv.v[it.l], bv[id][1]);
+      }
 #if defined(ECNF_SPLIT_IDENT_ACT)   // timing experiment: identity activation (split kept, SiLU arithmetic dropped)
       ev[id][0] = 1.0f;
       ev[id][1] = 1.0f;
@@ -427,13 +439,13 @@ __device__ __forceinline__ void chain_split(SplitX<NF>& XA, SplitX<NF>& XB, f32x
         e2v[id][0] = __builtin_amdgcn_exp2f(dv[id][0]);
         e2v[id][1] = __builtin_amdgcn_exp2f(dv[id][1]);
       } else if constexpr (NT) {
-#ifdef ECNF_CHAIN_BIAS_INIT
-        dv[id][0] = accT[it.j][r];
-        dv[id][1] = accT[it.j][r + 1];
-#else
-        dv[id][0] = accT[it.j][r] * inv.v[it.l];
-        dv[id][1] = accT[it.j][r + 1] * inv.v[it.l];
-#endif
+        if constexpr (kBI) {
+          dv[id][0] = accT[it.j][r];
+          dv[id][1] = accT[it.j][r + 1];
+        } else {
+          dv[id][0] = accT[it.j][r] * inv.v[it.l];
+          dv[id][1] = accT[it.j][r + 1] * inv.v[it.l];
+        }
       }
     }); };
     // stage B
@@ -547,18 +559,16 @@ __device__ __forceinline__ void chain_split(SplitX<NF>& XA, SplitX<NF>& XB, f32x
     if constexpr (mfma_group) {
       // schedule: weight loads, bias reads, then MFMA / VALU alternating
       constexpr int nvalu = (4 + 2 * NT) * nA + 4 * nB + (3 + 11 * NT) * nC;
-      constexpr int nmfma = kTerms * (1 + NT);
+      constexpr int nmfma = kTerms * (1 + NT) + (WP == 3 ? 1 : 0);
       constexpr int per = (nvalu + nmfma - 1) / nmfma;
 #ifndef ECNF_SPLIT_NO_SGB
 #if defined(ECNF_SPLIT_WLDS)
       if constexpr (gg + PF < G) __builtin_amdgcn_sched_group_barrier(0x100, kPieces, 0);
 #elif !defined(ECNF_SPLIT_NO_WLOAD)
-      if constexpr (gg + PF < G) __builtin_amdgcn_sched_group_barrier(0x020, kPieces, 0);
+      if constexpr (gg + PF < G) __builtin_amdgcn_sched_group_barrier(0x020, WP, 0);
 #endif
       if constexpr (nbias > 0) __builtin_amdgcn_sched_group_barrier(0x100, nbias, 0);
-#ifdef ECNF_CHAIN_BIAS_INIT
       if constexpr (load_cb) __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
-#endif
       static_for<nmfma>([&](auto) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
         if constexpr (per > 0) __builtin_amdgcn_sched_group_barrier(0x002, per, 0);
@@ -583,11 +593,11 @@ __device__ __forceinline__ void chain_split(SplitX<NF>& XA, SplitX<NF>& XB, f32x
 }
 
 // primal-only chain (the tangent arguments alias the primal ones and are never touched)
-template <int NF, int NL>
+template <int NF, int NL, int WP = kPieces>
 __device__ __forceinline__ void chain_split(SplitX<NF>& XA, SplitX<NF>& XB, f32x16 (&acc)[NF],
                                             const unsigned* __restrict__ Wpk, const float* __restrict__ bias,
                                             const ChainInv& inv, int lane) {
-  chain_split<NF, NL, 0>(XA, XB, acc, Wpk, bias, inv, lane, XA, XB, acc);
+  chain_split<NF, NL, 0, WP>(XA, XB, acc, Wpk, bias, inv, lane, XA, XB, acc);
 }
 
 // the tangent kernels' chain segment on natural-domain fp32 activations (fp32-MFMA accumulator layout, as
@@ -606,7 +616,7 @@ __device__ __forceinline__ void chain_split_tangent(f32x16 (&X)[NF], f32x16 (&XT
       put_pair<NF, fb, 2 * i>(XAT, kNegLog2e * XT[fb][2 * i], kNegLog2e * XT[fb][2 * i + 1]);
     });
   });
-  chain_split<NF, NL, 1>(XA, XB, X, Wpk, bias, inv, lane, XAT, XBT, XT);
+  chain_split<NF, NL, 1, 3>(XA, XB, X, Wpk, bias, inv, lane, XAT, XBT, XT);
 #pragma unroll
   for (int fb = 0; fb < NF; ++fb)
 #pragma unroll
@@ -639,42 +649,34 @@ __device__ __forceinline__ void split_blocks(const f32x16 (&X)[NF], SplitX<NF>& 
   });
 }
 
-// one pass of one layer: acc[jb] = (BIAS ? b' : 0) + sum over (fb, u) of W[l][jb][fb][u] X'[fb][u]
-template <int NF, bool BIAS>
+// weight groups in flight in dual_pass: 3 pieces x (PF + 1) slots beside the split input, the accumulators and the
+// other operand's fp32 activations (512-register waves)
+#ifndef ECNF_DUAL_PF
+#define ECNF_DUAL_PF 2
+#endif
+// one pass of one layer over the 3-piece exact weights (chain_split WP = 3): acc[jb] = sum over (fb, u) of
+// W[l][jb][fb][u] X'[fb][u] with the w2 x0 term in the PRIMAL pass (the tangent pass keeps three terms)
+template <int NF, bool PRIMAL>
 __device__ __forceinline__ void dual_pass(const SplitX<NF>& X, f32x16 (&acc)[NF], __amdgpu_buffer_rsrc_t rsrc,
-                                          int voff, int layer_soff, const float* __restrict__ lbias) {
-  constexpr int G = 2 * NF * NF, PF = ECNF_SPLIT_PF;
-  u32x4 wbuf[PF + 1][kPieces];
+                                          int voff, int layer_soff) {
+  constexpr int G = 2 * NF * NF, PF = ECNF_DUAL_PF, WP = 3;
+  u32x4 wbuf[PF + 1][WP];
   static_for<PF>([&](auto Gc) {
     constexpr int gg = decltype(Gc)::value;
 #pragma unroll
-    for (int p = 0; p < kPieces; ++p) wbuf[gg][p] = wload(rsrc, voff, layer_soff + (gg * kPieces + p) * kPieceBytes);
+    for (int p = 0; p < WP; ++p) wbuf[gg][p] = wload(rsrc, voff, layer_soff + (gg * WP + p) * kPieceBytes);
   });
   static_for<G>([&](auto Gc) {
     constexpr int gg = decltype(Gc)::value;
     constexpr int jb = gg / (2 * NF), fb = (gg % (2 * NF)) >> 1, u = gg & 1;
     if constexpr (gg + PF < G) {
 #pragma unroll
-      for (int p = 0; p < kPieces; ++p)
-        wbuf[(gg + PF) % (PF + 1)][p] = wload(rsrc, voff, layer_soff + ((gg + PF) * kPieces + p) * kPieceBytes);
+      for (int p = 0; p < WP; ++p)
+        wbuf[(gg + PF) % (PF + 1)][p] = wload(rsrc, voff, layer_soff + ((gg + PF) * WP + p) * kPieceBytes);
     }
-    if constexpr (fb == 0 && u == 0) {
-      if constexpr (BIAS) {
-        f32x16 c;
-        static_for<4>([&](auto Qc) {
-          constexpr int q = decltype(Qc)::value;
-          const f32x4 b4 = *reinterpret_cast<const f32x4*>(lbias + jb * 32 + 8 * q);
-          c[4 * q] = b4[0];
-          c[4 * q + 1] = b4[1];
-          c[4 * q + 2] = b4[2];
-          c[4 * q + 3] = b4[3];
-        });
-        acc[jb] = c;
-      } else {
-        acc[jb] = f32x16{};
-      }
-    }
+    if constexpr (fb == 0 && u == 0) acc[jb] = f32x16{};
     const u32x4* A = wbuf[gg % (PF + 1)];
+    if constexpr (PRIMAL) acc[jb] = mfma_split(A[2], X.v[fb][u][0], acc[jb]);
     static_for<kTerms>([&](auto Tc) {
       constexpr int t = decltype(Tc)::value;
       acc[jb] = mfma_split(A[term_w(t)], X.v[fb][u][term_x(t)], acc[jb]);
@@ -685,8 +687,10 @@ __device__ __forceinline__ void dual_pass(const SplitX<NF>& X, f32x16 (&acc)[NF]
 
 template <int NF, int NL>
 __device__ __forceinline__ void chain_dual_seq(f32x16 (&X)[NF], f32x16 (&XT)[NF], const unsigned* __restrict__ Wpk,
-                                               const float* __restrict__ bias, int lane, bool in_log2) {
+                                               const float* __restrict__ bias, const float* cinv, int lane,
+                                               bool in_log2) {
   constexpr float kNegLog2e = -1.4426950408889634f, kNegLn2 = -0.69314718055994531f;
+  constexpr int WP = 3;   // exact 3-piece weights (chain_split WP = 3)
   const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned*>(Wpk), (short)0,
                                                                          0x7fffffff, 0x00020000);
   const int voff = lane * 16;
@@ -702,30 +706,38 @@ __device__ __forceinline__ void chain_dual_seq(f32x16 (&X)[NF], f32x16 (&XT)[NF]
   }
   // a runtime layer loop with scheduling fences between the phases: only one pass's operands are live at a time
   for (int l = 0; l < NL; ++l) {
-    const int soff = l * (2 * NF * NF) * kPieces * kPieceBytes;
+    const int soff = l * (2 * NF * NF) * WP * kPieceBytes;
     {
       SplitX<NF> XA;
       split_blocks<NF>(X, XA);
       __builtin_amdgcn_sched_barrier(0);
-      dual_pass<NF, true>(XA, X, rsrc, voff, soff, lbias + l * NF * 32);   // X <- u (primal pre-activation)
+      dual_pass<NF, true>(XA, X, rsrc, voff, soff);    // X <- s W X' (primal, exact weights)
     }
     __builtin_amdgcn_sched_barrier(0);
     {
       SplitX<NF> XAT;
       split_blocks<NF>(XT, XAT);
       __builtin_amdgcn_sched_barrier(0);
-      dual_pass<NF, false>(XAT, XT, rsrc, voff, soff, nullptr);           // XT <- du
+      dual_pass<NF, false>(XAT, XT, rsrc, voff, soff);  // XT <- s W X'_T
     }
     __builtin_amdgcn_sched_barrier(0);
+    const float il = cinv[l];   // 1 / the layer's weight scale (read where used: nothing live across the passes)
+    const float* lb = lbias + l * NF * 32;
 #pragma unroll
     for (int fb = 0; fb < NF; ++fb)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float u = X[fb][r];
-        const float rr = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(u));
-        const float y = u * rr;
-        X[fb][r] = y;
-        XT[fb][r] = rr * XT[fb][r] * fmaf(u - y, kNegLn2, 1.0f);
+      for (int q = 0; q < 4; ++q) {
+        // the biases of registers 4q .. 4q+3 (rows acc_row(r, kk) = 8q + 4kk + 0..3): one 16-B LDS read
+        const f32x4 b4 = *reinterpret_cast<const f32x4*>(lb + fb * 32 + 8 * q);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = 4 * q + i;
+          const float u = fmaf(X[fb][r], il, b4[i]);   // u = W X' + b'
+          const float rr = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(u));
+          const float y = u * rr;
+          X[fb][r] = y;
+          XT[fb][r] = rr * (XT[fb][r] * il) * fmaf(u - y, kNegLn2, 1.0f);
+        }
       }
     __builtin_amdgcn_sched_barrier(0);
   }

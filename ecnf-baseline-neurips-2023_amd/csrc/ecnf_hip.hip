@@ -10,9 +10,11 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstddef>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -237,6 +239,8 @@ size_t param_count(const ecnf_cfg& c) {
 
 }  // namespace
 
+static_assert(sizeof(Net) <= 4096, "Net is passed by value as a kernel argument");
+
 struct ecnf_handle {
   ecnf_cfg cfg;
   int device;
@@ -245,8 +249,16 @@ struct ecnf_handle {
   Net net[4];          // [2 P + NT], at the LDS-optimal molecules per workgroup (choose_mpw)
   size_t lds[4];       // dynamic LDS bytes per workgroup [2 P + NT]
   int ncu;             // compute units of the device (batch-aware workgroup sizing, net_for_batch)
-  float* pcache;       // exact trace: primal-aggregate cache of the sparse blocks (SolveP::pcache), grown on demand
-  size_t pcache_floats;
+  int exact_form;      // ecnf_exact_form (A/B diagnostics; ECNF_EXACT_FORM_DEFAULT in the product)
+  bool split_ok;       // the split-fp16 kernels can represent the weights (else the handle is strict fp32 only)
+  // ecnf_reserve_workspace: the arena ecnf_integrate uses for the exact trace's primal-aggregate cache
+  // (SolveP::pcache); never (re)allocated inside a solve call.  Calls on different streams are ordered by arena_ev.
+  float* arena;
+  size_t arena_bytes;
+  std::mutex arena_mu;
+  hipEvent_t arena_ev;
+  bool arena_used;
+  hipStream_t arena_stream;
 };
 
 namespace {
@@ -348,6 +360,36 @@ static void pack_split_layer(const float* W, int M, float scale, uint32_t* dst) 
       }
 }
 
+// the divergence kernels' exact chain weights (chain_split WP = 3): w s = h0 + h1 + h2 in fp16 pieces, exact for every
+// weight within 2^-5 of the layer's largest (the differences are exact in fp32; below that h2 is an fp16 subnormal,
+// |error| <= 2^-25 in scaled units, i.e. <= 2^-37 of the largest weight).  Layout as pack_split_layer with 3 pieces:
+// [group][piece][lane][4 u32]
+static void pack_split_layer3(const float* W, int M, float scale, uint32_t* dst) {
+  const int NF = M / 32;
+  for (int jb = 0; jb < NF; ++jb)
+    for (int fb = 0; fb < NF; ++fb)
+      for (int u = 0; u < 2; ++u) {
+        const int g = (jb * NF + fb) * 2 + u;
+        for (int l = 0; l < 64; ++l)
+          for (int j = 0; j < 8; ++j) {
+            const int r = 8 * u + j, h = l >> 5;
+            const int in = 32 * fb + (r & 3) + 8 * (r >> 2) + 4 * h, out = 32 * jb + (l & 31);
+            const float ws = W[(size_t)in * M + out] * scale;
+            const _Float16 h0 = (_Float16)ws;
+            const float r1 = ws - (float)h0;
+            const _Float16 h1 = (_Float16)r1;
+            const _Float16 h2 = (_Float16)(r1 - (float)h1);
+            const _Float16 hp[3] = {h0, h1, h2};
+            for (int p = 0; p < 3; ++p) {
+              uint16_t bits;
+              std::memcpy(&bits, &hp[p], 2);
+              uint32_t& word = dst[(((size_t)g * 3 + p) * 64 + l) * 4 + (j >> 1)];
+              word = (j & 1) ? ((word & 0x0000ffffu) | ((uint32_t)bits << 16)) : ((word & 0xffff0000u) | bits);
+            }
+          }
+      }
+}
+
 struct HostBlock {
   const float *xb, *xk, *gb, *gk;
   const float *eb[4], *ek[4];
@@ -404,8 +446,14 @@ void set_mpw(Net& n, const ecnf_cfg& c, int NT, int P, int mpw, int rp) {
 int choose_mpw(const ecnf_cfg& c, int NT, int P, int* mpw_out, size_t* lds_out, int* rp_out) {
   const int N = c.n_nodes, D = c.dim, H = c.hidden, T = c.time_embedding_dim, M = c.mlp_width;
   const int E = N * (N - 1);
-  const char* env = std::getenv(NT ? "ECNF_MPW_TANGENT" : "ECNF_MPW");
-  const int forced = env ? std::atoi(env) : 0;
+  // experiment builds only (tools/build_timing.sh DEVFLAGS): -DECNF_FORCE_MPW / -DECNF_FORCE_MPW_TANGENT
+#ifndef ECNF_FORCE_MPW
+#define ECNF_FORCE_MPW 0
+#endif
+#ifndef ECNF_FORCE_MPW_TANGENT
+#define ECNF_FORCE_MPW_TANGENT 0
+#endif
+  const int forced = NT ? ECNF_FORCE_MPW_TANGENT : ECNF_FORCE_MPW;
   double best = -1;
   int best_m = 0;
   size_t best_lds = 0;
@@ -460,16 +508,13 @@ bool shape_supported(const ecnf_cfg& c, int NT, int P = -1) {
 // on m (every molecule owns its edge tiles and node rows), so results are bitwise independent of the choice.
 // Adaptive solves: a workgroup runs until its slowest molecule is done, and workgroups of unequal length balance
 // over the CUs as they retire, so the model charges (workgroups / CUs) continuous rounds, plus a per-workgroup
-// penalty per extra molecule for the expected max of m step counts (ECNF_ADAPTIVE_MPW_PENALTY, default 0: measured
-// on ALDP B = 512 PID, penalty 0 / 0.15 / 0.3 -> sample 3.23 / 3.73 / 3.70 ms, Hutchinson log_prob 57.9 / 58.0 /
-// 58.1 ms, profiles/round2/mpw_ab.log).
-double adaptive_penalty() {
-  static const double v = [] {
-    const char* e = std::getenv("ECNF_ADAPTIVE_MPW_PENALTY");
-    return e ? std::atof(e) : 0.0;
-  }();
-  return v;
-}
+// penalty per extra molecule for the expected max of m step counts (0: measured on ALDP B = 512 PID, penalty
+// 0 / 0.15 / 0.3 -> sample 3.23 / 3.73 / 3.70 ms, Hutchinson log_prob 57.9 / 58.0 / 58.1 ms,
+// profiles/round2/mpw_ab.log; -DECNF_ADAPTIVE_MPW_PENALTY=x in experiment builds).
+#ifndef ECNF_ADAPTIVE_MPW_PENALTY
+#define ECNF_ADAPTIVE_MPW_PENALTY 0.0
+#endif
+constexpr double adaptive_penalty() { return ECNF_ADAPTIVE_MPW_PENALTY; }
 
 Net net_for_batch(const ecnf_handle* h, int ix, int B, size_t* lds, bool adaptive = false) {
   Net n = h->net[ix];
@@ -545,6 +590,33 @@ hipError_t dispatch_vf(const ecnf_handle* h, int NT, const float* x, const float
   return hipErrorInvalidValue;
 }
 
+// Does an exact-trace solve on this handle run the sparse blocks 1 and K (egnn_eval sparse_a)?  Only the kernels that
+// compile them (egnn_eval kSparseX: the M <= 128 split tangent kernels except the L = 2 shapes (128, *, *) and
+// (*, 2, 2)), and only where a molecule has >= 3 edge tiles per dual tile (LJ13: 5 vs 1, ALDP: 15 vs 2; not DW4).
+bool exact_sparse(const ecnf_handle* h, int divergence) {
+  const ecnf_cfg& c = h->cfg;
+  if (divergence != ECNF_DIV_EXACT || h->prec != ECNF_PREC_SPLIT_F16 || c.mlp_width > 128) return false;
+  if (c.mlp_depth == 2 && (c.mlp_width == 128 || c.dim == 2)) return false;
+  const int nn1 = c.n_nodes - 1, tpm = (c.n_nodes * nn1 + 31) / 32, ndt = (2 * nn1 + 31) / 32;
+  return tpm >= 3 * ndt;
+}
+
+// floats of one molecule slot of the primal-aggregate cache: block 1's message sums [N][M] and the shift sums of
+// blocks 1 and K [2][N][D] (egnn_eval, pcache)
+size_t pcache_stride(const ecnf_handle* h) {
+  const ecnf_cfg& c = h->cfg;
+  return (size_t)c.n_nodes * c.mlp_width + 2 * (size_t)c.n_nodes * c.dim;
+}
+
+// slots of a batch: the grid covers ceil(B / m) m <= B + MPW - 1 molecule slots (m <= MPW, net_for_batch)
+size_t pcache_floats(const ecnf_handle* h, int batch) {
+  return (size_t)(batch + h->net[2 * h->prec + 1].MPW) * pcache_stride(h);
+}
+
+int integrate_impl(ecnf_handle* h, const ecnf_solve_opts* o, const float* y0, const int32_t* feat, const float* eps,
+                   float* y1, float* dlogp, int32_t* nfe, int32_t* status, int32_t batch, float* ws, size_t ws_bytes,
+                   hipStream_t stream, bool arena);
+
 }  // namespace
 
 // =====================================================================================================
@@ -586,6 +658,55 @@ int ecnf_debug_stamps(unsigned long long* out, int n, int reset) {
 #endif
 
 const char* ecnf_last_error(void) { return g_err.c_str(); }
+
+int ecnf_struct_layout(int32_t which, size_t* out, int32_t cap) {
+#define L_(T, f) offsetof(T, f)
+  size_t v[16];
+  int n = 0;
+  switch (which) {
+    case 0: {
+      const size_t o[] = {sizeof(ecnf_cfg), L_(ecnf_cfg, n_nodes), L_(ecnf_cfg, dim), L_(ecnf_cfg, n_features),
+                          L_(ecnf_cfg, hidden), L_(ecnf_cfg, time_embedding_dim), L_(ecnf_cfg, mlp_width),
+                          L_(ecnf_cfg, mlp_depth), L_(ecnf_cfg, n_blocks), L_(ecnf_cfg, base_scale),
+                          L_(ecnf_cfg, normalization_constant)};
+      n = sizeof(o) / sizeof(o[0]);
+      std::memcpy(v, o, sizeof(o));
+      break;
+    }
+    case 1: {
+      const size_t o[] = {sizeof(ecnf_solve_opts), L_(ecnf_solve_opts, solver), L_(ecnf_solve_opts, divergence),
+                          L_(ecnf_solve_opts, t0), L_(ecnf_solve_opts, t1), L_(ecnf_solve_opts, dt0),
+                          L_(ecnf_solve_opts, rtol), L_(ecnf_solve_opts, atol), L_(ecnf_solve_opts, dtmin),
+                          L_(ecnf_solve_opts, max_steps)};
+      n = sizeof(o) / sizeof(o[0]);
+      std::memcpy(v, o, sizeof(o));
+      break;
+    }
+    case 2: {
+      const size_t o[] = {sizeof(ecnf_target), L_(ecnf_target, kind), L_(ecnf_target, n_nodes), L_(ecnf_target, dim),
+                          L_(ecnf_target, epsilon), L_(ecnf_target, tau), L_(ecnf_target, r),
+                          L_(ecnf_target, harmonic_coef), L_(ecnf_target, a), L_(ecnf_target, b), L_(ecnf_target, c),
+                          L_(ecnf_target, d0), L_(ecnf_target, r_nodes)};
+      n = sizeof(o) / sizeof(o[0]);
+      std::memcpy(v, o, sizeof(o));
+      break;
+    }
+    case 3: {
+      const size_t o[] = {sizeof(ecnf_adam_opts), L_(ecnf_adam_opts, lr), L_(ecnf_adam_opts, b1),
+                          L_(ecnf_adam_opts, b2), L_(ecnf_adam_opts, eps), L_(ecnf_adam_opts, eps_root),
+                          L_(ecnf_adam_opts, count), L_(ecnf_adam_opts, ema_beta)};
+      n = sizeof(o) / sizeof(o[0]);
+      std::memcpy(v, o, sizeof(o));
+      break;
+    }
+    default:
+      return -1;
+  }
+#undef L_
+  for (int i = 0; i < n && i < cap; ++i)
+    if (out) out[i] = v[i];
+  return n - 1;
+}
 
 int ecnf_param_count(const ecnf_cfg* cfg, size_t* n_floats) {
   int rc = check_cfg(cfg);
@@ -636,9 +757,10 @@ int ecnf_create(const ecnf_cfg* cfg, const float* params, size_t n_floats, int d
 
   // ---- repack ----
   Packer pk;
+  bool split_ok = true;   // every edge-chain weight fits the unscaled fp16 split (|w| < 2^15)
   struct Off {
     size_t Wn, bn, Wp, bp, wd, We, Ws, be, wx, wg, Wh[kMaxPhiH], bh[kMaxPhiH], Wn_s, Wp_s, Wh_s[kMaxPhiH];
-    size_t bp_u, wd_u, be_u, wg_u, wx_u, Wh_sn0, W1_s;
+    size_t bp_u, wd_u, be_u, wg_u, wx_u, Wh_sn0, W1_s, Ws3;
     float bx, bg, hinv_n0, w1inv;
     float cinv[2 * 4 - 1], ninv, pinv, hinv[kMaxPhiH];
   };
@@ -708,18 +830,27 @@ int ecnf_create(const ecnf_cfg* cfg, const float* params, size_t n_floats, int d
 #ifdef ECNF_CHAIN_BIAS_INIT
       // unscaled pieces: the chain adds the bias through the accumulator (chain_split.hpp); fp16 piece 0 must not
       // overflow
+      // overflow: such a network runs on the strict-fp32 kernels only (split_ok = false, see below)
       float mx = 0.f;
       for (size_t i = 0; i < (size_t)M * M; ++i) mx = std::max(mx, std::fabs(W[i]));
-      if (!(mx < 32768.f))
-        return fail(ECNF_E_UNSUPPORTED, "edge-MLP weight magnitude >= 2^15 does not fit the unscaled fp16 split");
+      if (!(mx < 32768.f)) split_ok = false;
       const float sc = 1.0f;
 #else
       const float sc = split_scale(W, (size_t)M * M);
 #endif
-      o.cinv[cl] = 1.0f / sc;
+      o.cinv[cl] = 1.0f / split_scale(W, (size_t)M * M);   // the 3-piece chain's scale (Ws3); sc = 1 is not read
       pack_split_layer(W, M, sc, ws.data() + cl * split_layer);
     }
     o.Ws = pk.put(reinterpret_cast<const float*>(ws.data()), ws.size());
+    {   // the divergence kernels' exact 3-piece chain (scaled per layer)
+      const size_t layer3 = (size_t)2 * NF * NF * 3 * 256;
+      std::vector<uint32_t> ws3((size_t)nchain * layer3, 0u);
+      for (int cl = 0; cl < nchain; ++cl) {
+        const float* W = cl < L - 1 ? b.ek[cl + 1] : b.tk[cl - (L - 1)];
+        pack_split_layer3(W, M, 1.0f / o.cinv[cl], ws3.data() + cl * layer3);
+      }
+      o.Ws3 = pk.put(reinterpret_cast<const float*>(ws3.data()), ws3.size());
+    }
     o.be = pk.put(be.data(), be.size());
     o.be_u = pk.put(scaled(be.data(), be.size(), kNegLog2e).data(), be.size());
     o.wx = pk.put(b.xk, M);
@@ -759,7 +890,9 @@ int ecnf_create(const ecnf_cfg* cfg, const float* params, size_t n_floats, int d
   h->cfg = c;
   h->device = device;
   h->dbuf = dbuf;
-  h->prec = ECNF_PREC_SPLIT_F16;
+  // a network the split kernels cannot represent runs on the strict-fp32 kernels (ecnf_get_precision reports it)
+  h->split_ok = split_ok;
+  h->prec = split_ok ? ECNF_PREC_SPLIT_F16 : ECNF_PREC_FP32;
   {
     hipDeviceProp_t prop;
     h->ncu = hipGetDeviceProperties(&prop, device) == hipSuccess ? prop.multiProcessorCount : 256;
@@ -802,6 +935,7 @@ int ecnf_create(const ecnf_cfg* cfg, const float* params, size_t n_floats, int d
       w.hinv_n0 = o.hinv_n0;
       w.W1_s = reinterpret_cast<const unsigned*>(dbuf + o.W1_s);
       w.w1inv = o.w1inv;
+      w.Ws3 = reinterpret_cast<const unsigned*>(dbuf + o.Ws3);
     }
     int mpw = 0, rp = 0;
     size_t lds = 0;
@@ -846,6 +980,8 @@ int ecnf_update_params(ecnf_handle* h, const float* params, int32_t on_device) {
     h->net[i] = t->net[i];
     h->lds[i] = t->lds[i];
   }
+  h->split_ok = t->split_ok;
+  if (!h->split_ok) h->prec = ECNF_PREC_FP32;
   return ecnf_destroy(t);
 }
 
@@ -854,7 +990,8 @@ int ecnf_destroy(ecnf_handle* h) {
   HIP_TRY(hipSetDevice(h->device));
   HIP_TRY(hipDeviceSynchronize());
   HIP_TRY(hipFree(h->dbuf));
-  if (h->pcache) HIP_TRY(hipFree(h->pcache));
+  if (h->arena) HIP_TRY(hipFree(h->arena));
+  if (h->arena_ev) HIP_TRY(hipEventDestroy(h->arena_ev));
   delete h;
   return ECNF_OK;
 }
@@ -868,6 +1005,8 @@ int ecnf_molecules_per_workgroup(ecnf_handle* h, int32_t with_tangent, int32_t* 
 int ecnf_set_precision(ecnf_handle* h, int32_t precision) {
   if (!h) return fail(ECNF_E_INVALID, "NULL handle");
   if (precision != ECNF_PREC_SPLIT_F16 && precision != ECNF_PREC_FP32) return fail(ECNF_E_INVALID, "unknown precision");
+  if (precision == ECNF_PREC_SPLIT_F16 && !h->split_ok)
+    return fail(ECNF_E_UNSUPPORTED, "edge-MLP weights >= 2^15 in magnitude: this handle runs the strict-fp32 kernels only");
   h->prec = precision;
   return ECNF_OK;
 }
@@ -917,10 +1056,62 @@ int ecnf_vf_jvp(ecnf_handle* h, const float* x, const float* t, const int32_t* f
   return ECNF_OK;
 }
 
+int ecnf_integrate_workspace_size(ecnf_handle* h, const ecnf_solve_opts* o, int32_t batch, size_t* bytes) {
+  if (!h || !o || !bytes) return fail(ECNF_E_INVALID, "NULL argument");
+  if (batch < 0) return fail(ECNF_E_INVALID, "batch < 0");
+  *bytes = exact_sparse(h, o->divergence) ? pcache_floats(h, batch) * sizeof(float) : 0;
+  return ECNF_OK;
+}
+
+int ecnf_reserve_workspace(ecnf_handle* h, size_t bytes) {
+  if (!h) return fail(ECNF_E_INVALID, "NULL handle");
+  std::lock_guard<std::mutex> lk(h->arena_mu);
+  if (bytes <= h->arena_bytes) return ECNF_OK;
+  HIP_TRY(hipSetDevice(h->device));
+  HIP_TRY(hipDeviceSynchronize());   // no call is using the old arena
+  if (h->arena) HIP_TRY(hipFree(h->arena));
+  h->arena = nullptr;
+  h->arena_bytes = 0;
+  HIP_TRY(hipMalloc(&h->arena, bytes));
+  h->arena_bytes = bytes;
+  return ECNF_OK;
+}
+
+int ecnf_set_exact_form(ecnf_handle* h, int32_t form) {
+  if (!h) return fail(ECNF_E_INVALID, "NULL handle");
+  if (form < ECNF_EXACT_FORM_DEFAULT || form > ECNF_EXACT_FORM_SPARSE) return fail(ECNF_E_INVALID, "unknown exact form");
+  h->exact_form = form;
+  return ECNF_OK;
+}
+
+int ecnf_integrate_ws(ecnf_handle* h, const ecnf_solve_opts* o, const float* y0, const int32_t* feat, const float* eps,
+                      float* y1, float* dlogp, int32_t* nfe, int32_t* status, int32_t batch, void* workspace,
+                      size_t workspace_bytes, void* stream) {
+  if (!h || !o) return fail(ECNF_E_INVALID, "NULL handle/options");
+  if (batch < 0) return fail(ECNF_E_INVALID, "batch < 0");
+  if (workspace && batch > 0 && exact_sparse(h, o->divergence) &&
+      workspace_bytes < pcache_floats(h, batch) * sizeof(float))
+    return fail(ECNF_E_INVALID, "workspace smaller than ecnf_integrate_workspace_size");
+  return integrate_impl(h, o, y0, feat, eps, y1, dlogp, nfe, status, batch, (float*)workspace, workspace_bytes,
+                        (hipStream_t)stream, false);
+}
+
 int ecnf_integrate(ecnf_handle* h, const ecnf_solve_opts* o, const float* y0, const int32_t* feat, const float* eps,
                    float* y1, float* dlogp, int32_t* nfe, int32_t* status, int32_t batch, void* stream) {
   if (!h || !o) return fail(ECNF_E_INVALID, "NULL handle/options");
   if (batch < 0) return fail(ECNF_E_INVALID, "batch < 0");
+  // the handle's arena (ecnf_reserve_workspace) when it is large enough, else the uncached form (same results)
+  return integrate_impl(h, o, y0, feat, eps, y1, dlogp, nfe, status, batch, h->arena, h->arena_bytes,
+                        (hipStream_t)stream, true);
+}
+
+}  // extern "C"
+
+namespace {
+
+int integrate_impl(ecnf_handle* h, const ecnf_solve_opts* o, const float* y0, const int32_t* feat, const float* eps,
+                   float* y1, float* dlogp, int32_t* nfe, int32_t* status, int32_t batch, float* ws, size_t ws_bytes,
+                   hipStream_t stream, bool arena) {
   if (batch > 0 && (!y0 || !feat || !y1)) return fail(ECNF_E_INVALID, "NULL argument");
   if (o->solver != ECNF_SOLVER_EULER && o->solver != ECNF_SOLVER_DOPRI5) return fail(ECNF_E_INVALID, "unknown solver");
   if (o->divergence < ECNF_DIV_NONE || o->divergence > ECNF_DIV_EXACT) return fail(ECNF_E_INVALID, "unknown divergence");
@@ -949,38 +1140,40 @@ int ecnf_integrate(ecnf_handle* h, const ecnf_solve_opts* o, const float* y0, co
   sp.rtol = o->rtol;
   sp.atol = o->atol;
   sp.dtmin = o->dtmin;
-  // exact trace: block 1's sparse dual tiles (egnn_eval sparse_a) where a molecule has >= 3 edge tiles per dual tile
-  // (LJ13: 5 vs 1, ALDP: 15 vs 2; not DW4: 1 vs 1); kernels other than the M <= 128 split tangent kernels ignore it.
-  // ECNF_EXACT_SPARSE=0 turns it off (A/B and parity tests)
-  {
-    const int nn1 = h->cfg.n_nodes - 1, tpm = (h->cfg.n_nodes * nn1 + 31) / 32, ndt = (2 * nn1 + 31) / 32;
-    const char* env = std::getenv("ECNF_EXACT_SPARSE");
-    sp.sparse1 = (o->divergence == ECNF_DIV_EXACT && tpm >= 3 * ndt && !(env && std::atoi(env) == 0)) ? 1 : 0;
+  // exact trace: the sparse blocks 1 and K (egnn_eval sparse_a) where they pay (exact_sparse), and their primal
+  // aggregates cached over the JVP passes of an evaluation when a workspace of pcache_floats is given: the caller's
+  // (ecnf_integrate_ws) or the handle's arena (ecnf_integrate).  The three forms give bitwise equal results between
+  // the sparse and the cached form; ecnf_set_exact_form selects the others for A/B runs only.
+  sp.sparse1 = exact_sparse(h, o->divergence) && h->exact_form != ECNF_EXACT_FORM_ALL_DUAL ? 1 : 0;
+  sp.pcache = nullptr;
+  sp.pcache_slots = 0;
+  const size_t need = sp.sparse1 ? pcache_floats(h, batch) : 0;
+  const bool cached = sp.sparse1 && h->exact_form == ECNF_EXACT_FORM_DEFAULT && ws && ws_bytes >= need * sizeof(float);
+  if (cached) {
+    sp.pcache = ws;
+    sp.pcache_slots = (int)(ws_bytes / sizeof(float) / pcache_stride(h));
   }
   HIP_TRY(hipSetDevice(h->device));
-  // the primal-aggregate cache of the sparse blocks (one slot per molecule of the grid: <= batch + MPW - 1);
-  // ECNF_EXACT_PCACHE=0 turns it off (every JVP pass then recomputes the primal tiles)
-  sp.pcache = nullptr;
-  if (sp.sparse1) {
-    const char* env = std::getenv("ECNF_EXACT_PCACHE");
-    if (!(env && std::atoi(env) == 0)) {
-      const ecnf_cfg& c = h->cfg;
-      const size_t need = (size_t)(batch + h->net[2 * h->prec + 1].MPW) *
-                          ((size_t)c.n_nodes * c.mlp_width + 2 * (size_t)c.n_nodes * c.dim);
-      if (h->pcache_floats < need) {
-        if (h->pcache) HIP_TRY(hipFree(h->pcache));
-        h->pcache = nullptr;
-        h->pcache_floats = 0;
-        HIP_TRY(hipMalloc(&h->pcache, need * sizeof(float)));
-        h->pcache_floats = need;
-      }
-      sp.pcache = h->pcache;
-    }
+  if (cached && arena) {
+    // the arena is shared by every ecnf_integrate call on the handle: calls on different streams are ordered
+    // through an event (no host synchronisation), and the bookkeeping is guarded for calls from several threads
+    std::lock_guard<std::mutex> lk(h->arena_mu);
+    if (!h->arena_ev) HIP_TRY(hipEventCreateWithFlags(&h->arena_ev, hipEventDisableTiming));
+    if (h->arena_used && h->arena_stream != stream) HIP_TRY(hipStreamWaitEvent(stream, h->arena_ev, 0));
+    HIP_TRY(dispatch_integrate(h, NT, sp, y0, feat, eps, y1, dlogp, nfe, status, batch, stream));
+    HIP_TRY(hipEventRecord(h->arena_ev, stream));
+    h->arena_used = true;
+    h->arena_stream = stream;
+  } else {
+    HIP_TRY(dispatch_integrate(h, NT, sp, y0, feat, eps, y1, dlogp, nfe, status, batch, stream));
   }
-  HIP_TRY(dispatch_integrate(h, NT, sp, y0, feat, eps, y1, dlogp, nfe, status, batch, (hipStream_t)stream));
   g_err.clear();
   return ECNF_OK;
 }
+
+}  // namespace
+
+extern "C" {
 
 int ecnf_base_sample(ecnf_handle* h, const float* z, float* x0, int32_t batch, void* stream) {
   if (!h) return fail(ECNF_E_INVALID, "NULL handle");

@@ -45,8 +45,10 @@ struct SolveP {
   int sparse1;
   // exact trace with sparse1: per-molecule cache of the primal edge aggregates of blocks 1 and K ([molecule slot of
   // the grid][N M + 2 N D] floats), written by the first JVP pass of an evaluation and read by the other ND - D - 1
-  // (the primal is the same in every pass), which then run only the dual tiles of those blocks.  nullptr: off
+  // (the primal is the same in every pass), which then run only the dual tiles of those blocks.  nullptr: off.
+  // pcache_slots: molecule slots the buffer holds (>= grid x MPW; device-checked build: ECNF_DCHECK bit 6)
   float* pcache;
+  int pcache_slots;
 };
 
 // solver state in LDS, after the eval region
@@ -123,6 +125,7 @@ __device__ __forceinline__ void joint_field(const Net& net, const Lds& s, const 
     float* pc = sparse && sp.pcache
                     ? sp.pcache + (size_t)blockIdx.x * MPW * (net.N * (NF * 32) + 2 * net.N * D)
                     : nullptr;
+    ECNF_DCHECK(!pc || (int)(blockIdx.x + 1) * MPW <= sp.pcache_slots, 6);
     egnn_eval<NF, NT, L, D, P>(net, s, st.ys, st.ts, st.tin, st.vout, st.tout, st.active, sparse ? k / D : -1, pc,
                                k0 == 0 ? 1 : 2);
     if constexpr (NT) {

@@ -199,7 +199,10 @@ __global__ void k_prologue(Geom G, const float* __restrict__ x1, const float* __
   }
 }
 
-// hin = [h | temb] (h: embedding rows for block 0, else the previous block's output)
+// hin = [h | temb] (h: embedding rows for block 0, else the previous block's output).  An embedding id outside
+// [0, n_features) (device-resident features are not checked on the host: no sync on the call path) is never used as
+// an index: its row becomes NaN, so the loss and the gradient are NaN instead of silently reading past the params
+// (nn.Embed would fail on it); k_embed_bwd matches no vocabulary row for it.
 __global__ void k_hin(Geom G, const float* __restrict__ h, long ldh, const int32_t* __restrict__ feat,
                       const float* __restrict__ emb, const float* __restrict__ temb, float* hin) {
   const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -208,8 +211,16 @@ __global__ void k_hin(Geom G, const float* __restrict__ h, long ldh, const int32
   const long row = idx / W;
   const int c = (int)(idx - row * W);
   float v;
-  if (c < G.H) v = feat ? emb[(long)feat[row] * G.H + c] : h[row * ldh + c];
-  else v = temb[(row / G.N) * G.T + (c - G.H)];
+  if (c < G.H) {
+    if (feat) {
+      const int f = feat[row];
+      v = (f >= 0 && f < G.nfeat) ? emb[(long)f * G.H + c] : __builtin_nanf("");
+    } else {
+      v = h[row * ldh + c];
+    }
+  } else {
+    v = temb[(row / G.N) * G.T + (c - G.H)];
+  }
   hin[idx] = v;
 }
 

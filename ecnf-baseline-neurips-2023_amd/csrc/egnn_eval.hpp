@@ -139,6 +139,10 @@ struct BlockW {
   // M = 256 tangent kernels: phi_e.0 kernel [(2H+1)][M] x -log2(e) as split node fragments (edge_layer1_dual)
   const unsigned* W1_s;
   float w1inv;
+  // the divergence kernels' chain: every chain layer scaled by a power of two and split into THREE fp16 pieces that
+  // hold the fp32 weight exactly (chain_split WP = 3); 1 / the scales are cinv (the 2-piece chain Ws is unscaled and
+  // ignores them with ECNF_CHAIN_BIAS_INIT, and uses the same scales without it)
+  const unsigned* Ws3;
 };
 
 struct Net {
@@ -203,6 +207,7 @@ __device__ unsigned long long g_stamps[32];
 //   bit 0  LDS carve-up + solver state past the launch's dynamic LDS      bit 1  edge receiver / sender row out of range
 //   bit 2  edge tile past the workgroup's tiles                           bit 3  node-GEMM row tile past RP
 //   bit 4  stored segment part (cross row) out of range                    bit 5  molecule slot past the workgroup
+//   bit 6  exact-trace primal-cache slot past the caller's workspace (SolveP::pcache_slots)
 // ---------------------------------------------------------------------------------------------------
 #ifdef ECNF_DEVICE_CHECKS
 __device__ unsigned g_checks[64];
@@ -1075,7 +1080,9 @@ __device__ __forceinline__ void edge_layer1_dual(const Net& net, const BlockW& b
 //   amode 1 (block 1): the edges at atom a (receivers i < a with sender a, receiver a with its N - 1 senders in
 //                      graph.py order, receivers i > a with sender a)
 //   amode 2 (last block): the edges INTO atoms 0 and a (receiver 0's N - 1 edges, then receiver a's; a >= 1)
-template <int NF, int NT, int L, int D, int P>
+// WPP: weight pieces of the primal split chain (kSplit branch): 2 in the primal kernels, 3 (exact weights, as the
+// dual tiles' primal) for the exact trace's primal-only tiles inside the divergence kernels
+template <int NF, int NT, int L, int D, int P, int WPP = kPieces>
 __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, const Lds& s, int tile, int lane, bool agg,
                                           int a = -1, int part = 0, int amode = 1) {
   const int kk = lane >> 5, li = lane & 31;
@@ -1203,14 +1210,15 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
     });
     STAMP_LANE0(s, kStEdgeLayer1, t_sub);
     // phi_e layers 2..L
-    const unsigned* Ws = launder_uniform(bw.Ws);
+    const unsigned* Ws = launder_uniform(WPP == 3 ? bw.Ws3 : bw.Ws);
+    const float* ci = bw.cinv;
     ChainInv ie, ix;
     static_for<2 * 4 - 1>([&](auto Lc) {
       constexpr int l = decltype(Lc)::value;
-      ie.v[l] = l < L - 1 ? bw.cinv[l] : 1.0f;
-      ix.v[l] = l < L ? bw.cinv[L - 1 + l] : 1.0f;
+      ie.v[l] = l < L - 1 ? ci[l] : 1.0f;
+      ix.v[l] = l < L ? ci[L - 1 + l] : 1.0f;
     });
-    chain_split<NF, L - 1>(XA, XB, acc, Ws, s.vecs, ie, lane);
+    chain_split<NF, L - 1, WPP>(XA, XB, acc, Ws, s.vecs, ie, lane);
     STAMP_LANE0(s, kStEdgeChainE, t_sub);
     edge_tail<NF, NT, L, D>(net, bw, s, acc, acc, valid, rr, agg_dst, r, dr, length, dlength, lane, agg,
                             [&](f32x16 (&m)[NF], f32x16 (&)[NF]) {
@@ -1223,9 +1231,10 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
                                   put_pair<NF, fb, 2 * i>(XA, m[fb][2 * i], m[fb][2 * i + 1]);
                                 });
                               });
-                              const unsigned* Wx = launder_uniform(bw.Ws + (size_t)(L - 1) * SplitPlan<NF, 1>::GL * kGroupU32);
+                              const unsigned* Wx = launder_uniform((WPP == 3 ? bw.Ws3 : bw.Ws) +
+                                                                   (size_t)(L - 1) * SplitPlan<NF, 1>::GL * WPP * 256);
                               STAMP_LANE0(s, kStEdgePhiXIn, t_sub);
-                              chain_split<NF, L>(XA, XB, m, Wx, s.vecs + (L - 1) * NF * 32, ix, lane);
+                              chain_split<NF, L, WPP>(XA, XB, m, Wx, s.vecs + (L - 1) * NF * 32, ix, lane);
                               STAMP_LANE0(s, kStEdgePhiX, t_sub);
                             });
     STAMP_LANE0(s, kStEdgeTail, t_sub);
@@ -1274,14 +1283,14 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
       ie.v[l] = l < L - 1 ? bw.cinv[l] : 1.0f;
       ix.v[l] = l < L ? bw.cinv[L - 1 + l] : 1.0f;
     });
-    chain_split<NF, L - 1, 1>(XA, XB, X, launder_uniform(bw.Ws), s.vecs, ie, lane, XAT, XBT, XT);
+    chain_split<NF, L - 1, 1, 3>(XA, XB, X, launder_uniform(bw.Ws3), s.vecs, ie, lane, XAT, XBT, XT);
     STAMP_LANE0(s, kStEdgeChainE, t_sub);
     // the tail stays in the log2 domain as in the primal split kernels: gate / shift with the -ln2-folded w_g', w_x'
     // (staged in vecs), the aggregate's -ln2 / sqrt(N-1) in the split phi_h.0 weights, phi_x fed the messages as is
     edge_tail<NF, NT, L, D>(net, bw, s, X, XT, valid, rr, agg_dst, r, dr, length, dlength, lane, agg,
                             [&](f32x16 (&Y)[NF], f32x16 (&YT)[NF]) {
                               const unsigned* Wx =
-                                  launder_uniform(bw.Ws + (size_t)(L - 1) * SplitPlan<NF, 1>::GL * kGroupU32);
+                                  launder_uniform(bw.Ws3 + (size_t)(L - 1) * SplitPlan<NF, 1>::GL * 3 * 256);
                               static_for<NF>([&](auto Fc) {
                                 constexpr int fb = decltype(Fc)::value;
                                 static_for<8>([&](auto Ic) {
@@ -1290,7 +1299,8 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
                                   put_pair<NF, fb, 2 * i>(XAT, YT[fb][2 * i], YT[fb][2 * i + 1]);
                                 });
                               });
-                              chain_split<NF, L, 1>(XA, XB, Y, Wx, s.vecs + (L - 1) * NF * 32, ix, lane, XAT, XBT, YT);
+                              chain_split<NF, L, 1, 3>(XA, XB, Y, Wx, s.vecs + (L - 1) * NF * 32, ix, lane, XAT, XBT,
+                                                       YT);
                             },
                             a < 0);   // block-1 dual tiles of the exact trace store tangents only
     STAMP_LANE0(s, kStEdgeTail, t_sub);
@@ -1301,13 +1311,14 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
     f32x16 X[NF], XT[NF];
     edge_layer1_dual<NF>(net, bw, s, rr, rs, len2, dlen2, X, XT, lane);
     STAMP_LANE0(s, kStEdgeLayer1, t_sub);
-    chain_dual_seq<NF, L - 1>(X, XT, launder_uniform(bw.Ws), s.vecs, lane, true);
+    chain_dual_seq<NF, L - 1>(X, XT, launder_uniform(bw.Ws3), s.vecs, bw.cinv, lane, true);
     STAMP_LANE0(s, kStEdgeChainE, t_sub);
     edge_tail<NF, NT, L, D>(net, bw, s, X, XT, valid, rr, agg_dst, r, dr, length, dlength, lane, agg,
                             [&](f32x16 (&Y)[NF], f32x16 (&YT)[NF]) {
                               const unsigned* Wx =
-                                  launder_uniform(bw.Ws + (size_t)(L - 1) * SplitPlan<NF, 1>::GL * kGroupU32);
-                              chain_dual_seq<NF, L>(Y, YT, Wx, s.vecs + (L - 1) * NF * 32, lane, false);
+                                  launder_uniform(bw.Ws3 + (size_t)(L - 1) * SplitPlan<NF, 1>::GL * 3 * 256);
+                              chain_dual_seq<NF, L>(Y, YT, Wx, s.vecs + (L - 1) * NF * 32, bw.cinv + (L - 1), lane,
+                                                    false);
                             });
     STAMP_LANE0(s, kStEdgeTail, t_sub);
     return;
@@ -1353,12 +1364,12 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
       ie.v[l] = l < L - 1 ? bw.cinv[l] : 1.0f;
       ix.v[l] = l < L ? bw.cinv[L - 1 + l] : 1.0f;
     });
-    chain_split_tangent<NF, L - 1>(X, XT, launder_uniform(bw.Ws), s.vecs, ie, lane);
+    chain_split_tangent<NF, L - 1>(X, XT, launder_uniform(bw.Ws3), s.vecs, ie, lane);
     STAMP_LANE0(s, kStEdgeChainE, t_sub);
     edge_tail<NF, NT, L, D>(net, bw, s, X, XT, valid, rr, agg_dst, r, dr, length, dlength, lane, agg,
                             [&](f32x16 (&Y)[NF], f32x16 (&YT)[NF]) {
                               const unsigned* Wx =
-                                  launder_uniform(bw.Ws + (size_t)(L - 1) * SplitPlan<NF, 1>::GL * kGroupU32);
+                                  launder_uniform(bw.Ws3 + (size_t)(L - 1) * SplitPlan<NF, 1>::GL * 3 * 256);
                               chain_split_tangent<NF, L>(Y, YT, Wx, s.vecs + (L - 1) * NF * 32, ix, lane);
                             });
   } else {
@@ -1545,7 +1556,7 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
         const int tile = nth_active(q) * tpm + (v2 - q * tpm);
         if constexpr (kSparseX) {
           if (ndt) {
-            edge_tile<NF, 0, L, D, P>(net, bw, s, tile, elane, need_h);
+            edge_tile<NF, 0, L, D, P, 3>(net, bw, s, tile, elane, need_h);   // exact weights, as the dual tiles
             continue;
           }
         }

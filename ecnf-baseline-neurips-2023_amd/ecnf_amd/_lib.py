@@ -17,6 +17,7 @@ PREC_SPLIT_F16, PREC_FP32 = 0, 1
 SOLVER_EULER, SOLVER_DOPRI5 = 0, 1
 DIV_NONE, DIV_HUTCHINSON, DIV_EXACT = 0, 1, 2
 CHAIN_FP32_MFMA, CHAIN_SPLIT_BF16, CHAIN_SPLIT_F16 = 0, 1, 2
+EXACT_FORM_DEFAULT, EXACT_FORM_ALL_DUAL, EXACT_FORM_SPARSE = 0, 1, 2
 
 # every symbol include/ecnf.h declares
 EXPORTED_SYMBOLS = (
@@ -24,7 +25,8 @@ EXPORTED_SYMBOLS = (
     "ecnf_vector_field", "ecnf_vf_jvp", "ecnf_integrate", "ecnf_base_sample", "ecnf_base_log_prob",
     "ecnf_molecules_per_workgroup", "ecnf_chain_arithmetic", "ecnf_target_log_prob", "ecnf_lse_partials",
     "ecnf_set_precision", "ecnf_get_precision", "ecnf_trainer_create", "ecnf_trainer_destroy", "ecnf_fm_loss_grad",
-    "ecnf_adam_update", "ecnf_update_params",
+    "ecnf_adam_update", "ecnf_update_params", "ecnf_integrate_workspace_size", "ecnf_integrate_ws",
+    "ecnf_reserve_workspace", "ecnf_set_exact_form", "ecnf_struct_layout",
 )
 
 TARGET_LJ, TARGET_DW = 0, 1
@@ -88,6 +90,19 @@ class EcnfAdamOpts(ctypes.Structure):
     ]
 
 
+# the ABI structs in ecnf_struct_layout's `which` order
+ABI_STRUCTS = (EcnfCfg, EcnfSolveOpts, EcnfTarget, EcnfAdamOpts)
+
+
+def struct_layout(which: int):
+    """(sizeof, [field offsets]) of ABI struct `which` as the compiled library lays it out."""
+    buf = (ctypes.c_size_t * 16)()
+    n = load().ecnf_struct_layout(which, buf, 16)
+    if n < 0:
+        raise ValueError(f"unknown struct {which}")
+    return buf[0], list(buf[1:1 + n])
+
+
 class EcnfError(RuntimeError):
     def __init__(self, code: int, msg: str):
         super().__init__(f"ecnf error {code}: {msg}")
@@ -134,6 +149,11 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
         "ecnf_fm_loss_grad": ([P, P, P, P, P, P, ctypes.c_float, I32, P, P, P], ctypes.c_int),
         "ecnf_adam_update": ([P, P, P, P, P, P, SZ, ctypes.POINTER(EcnfAdamOpts), P, P], ctypes.c_int),
         "ecnf_update_params": ([P, P, I32], ctypes.c_int),
+        "ecnf_integrate_workspace_size": ([P, ctypes.POINTER(EcnfSolveOpts), I32, ctypes.POINTER(SZ)], ctypes.c_int),
+        "ecnf_integrate_ws": ([P, ctypes.POINTER(EcnfSolveOpts), P, P, P, P, P, P, P, I32, P, SZ, P], ctypes.c_int),
+        "ecnf_reserve_workspace": ([P, SZ], ctypes.c_int),
+        "ecnf_set_exact_form": ([P, I32], ctypes.c_int),
+        "ecnf_struct_layout": ([I32, ctypes.POINTER(SZ), I32], ctypes.c_int),
     }
     for name, (argtypes, restype) in sig.items():
         fn = getattr(lib, name)

@@ -83,6 +83,9 @@ def device_params(params: Params, cfg: CNFConfig, device: torch.device) -> EcnfH
     if len(_HANDLE_CACHE) >= _CACHE_MAX:
         _HANDLE_CACHE.pop(next(iter(_HANDLE_CACHE)))   # freed by its __del__ once no caller holds it
     _HANDLE_CACHE[key] = h
+    # a caller that changes this handle (update_params / set_precision, e.g. on the handle of cnf.to_device(p) in a
+    # training loop) takes it out of the cache: a later apply(p, ...) uploads p again instead of using other weights
+    h._on_mutate.append(lambda: _HANDLE_CACHE.pop(key, None) if _HANDLE_CACHE.get(key) is h else None)
     return h
 
 

@@ -77,24 +77,50 @@ class EcnfHandle:
         _lib.check(self.lib.ecnf_create(ctypes.byref(self._c), blob.ctypes.data, blob.size, self.device.index,
                                         ctypes.byref(h)))
         self._h = h
-        self.set_precision(precision)
+        # callbacks run when this handle's weights or precision change (ecnf_amd.cnf evicts its content-hash cache
+        # entry, so a params dict never maps to a handle holding other weights)
+        self._on_mutate = []
+        cur = ctypes.c_int32()
+        _lib.check(self.lib.ecnf_get_precision(self._h, ctypes.byref(cur)))
+        if precision == "split_f16" and cur.value == _lib.PREC_FP32:
+            # edge-MLP weights >= 2^15 do not fit the fp16 split: ecnf_create made this a strict-fp32 handle
+            self.precision = "fp32"
+        else:
+            self._set_precision(precision)
+
+    def _mutated(self) -> None:
+        for cb in self._on_mutate:
+            cb()
+        self._on_mutate = []
 
     def update_params(self, params) -> None:
         """Re-pack new weights into this handle (ecnf_update_params): a flax-path dict / flat host blob, or the flat
         device tensor of a TrainingState."""
+        self._mutated()
         if torch.is_tensor(params) and params.is_cuda:
             p = params.to(self.device, torch.float32).contiguous().reshape(-1)
             if p.numel() != param_count(self.cfg):
                 raise ValueError(f"params blob has {p.numel()} floats, expected {param_count(self.cfg)}")
             _lib.check(self.lib.ecnf_update_params(self._h, p.data_ptr(), 1))
+            self._sync_precision()
             return
         blob = params if isinstance(params, np.ndarray) else flatten_params(params, self.cfg)
         blob = np.ascontiguousarray(blob, dtype=np.float32)
         if blob.size != param_count(self.cfg):
             raise ValueError(f"params blob has {blob.size} floats, expected {param_count(self.cfg)}")
         _lib.check(self.lib.ecnf_update_params(self._h, blob.ctypes.data, 0))
+        self._sync_precision()
+
+    def _sync_precision(self) -> None:
+        cur = ctypes.c_int32()
+        _lib.check(self.lib.ecnf_get_precision(self._h, ctypes.byref(cur)))
+        self.precision = "fp32" if cur.value == _lib.PREC_FP32 else "split_f16"
 
     def set_precision(self, precision: str) -> None:
+        self._mutated()
+        self._set_precision(precision)
+
+    def _set_precision(self, precision: str) -> None:
         if precision not in PRECISIONS:
             raise ValueError(f"precision must be one of {sorted(PRECISIONS)}")
         _lib.check(self.lib.ecnf_set_precision(self._h, PRECISIONS[precision]))
@@ -150,11 +176,11 @@ class EcnfHandle:
     def _fp32_available(self, with_tangent: bool) -> bool:
         """Whether the strict-fp32 kernels exist for this shape (the M = 256 tangent kernels are split-fp16 only)."""
         prev = self.precision
-        self.set_precision("fp32")
+        self._set_precision("fp32")
         try:
             return self.molecules_per_workgroup(with_tangent) > 0
         finally:
-            self.set_precision(prev)
+            self._set_precision(prev)
 
     def chain_arithmetic(self, with_tangent: bool = False) -> str:
         """Edge-chain arithmetic at the current precision: 'split_f16' (2-piece fp16 split, 3 cross terms),
@@ -219,12 +245,12 @@ class EcnfHandle:
                 if fallback and self.precision == "split_f16" and bool((st == _lib.ECNF_E_NONFINITE).any()) and \
                         self._fp32_available(divergence != _lib.DIV_NONE):
                     idx = torch.nonzero(status == _lib.ECNF_E_NONFINITE).reshape(-1)
-                    self.set_precision("fp32")
+                    self._set_precision("fp32")
                     try:
                         r = self._integrate(y0[idx].contiguous(), f[idx].contiguous(),
                                             None if e is None else e[idx].contiguous(), t0, t1, opts, divergence)
                     finally:
-                        self.set_precision("split_f16")
+                        self._set_precision("split_f16")
                     y1[idx], nfe[idx], status[idx] = r[0], r[2], r[3]
                     if dl is not None:
                         dl[idx] = r[1]
@@ -247,9 +273,23 @@ class EcnfHandle:
         nfe = torch.empty(B, device=self.device, dtype=torch.int32)
         status = torch.empty(B, device=self.device, dtype=torch.int32)
         o = opts.to_c(t0, t1, divergence)
-        _lib.check(self.lib.ecnf_integrate(self._h, ctypes.byref(o), _ptr(y0), _ptr(f), _ptr(e), _ptr(y1), _ptr(dl),
-                                           _ptr(nfe), _ptr(status), B, _stream(self.device)))
+        # the exact trace's primal-aggregate cache: a caller-owned workspace from torch's stream-ordered caching
+        # allocator (ecnf_integrate_ws), so concurrent solves on one handle never share it and the call allocates
+        # nothing itself
+        nbytes = ctypes.c_size_t(0)
+        _lib.check(self.lib.ecnf_integrate_workspace_size(self._h, ctypes.byref(o), B, ctypes.byref(nbytes)))
+        ws = torch.empty(nbytes.value, device=self.device, dtype=torch.uint8) if nbytes.value else None
+        _lib.check(self.lib.ecnf_integrate_ws(self._h, ctypes.byref(o), _ptr(y0), _ptr(f), _ptr(e), _ptr(y1), _ptr(dl),
+                                              _ptr(nfe), _ptr(status), B, _ptr(ws), nbytes.value,
+                                              _stream(self.device)))
         return y1, dl, nfe, status
+
+    def set_exact_form(self, form: str) -> None:
+        """A/B diagnostic of the exact trace (ecnf_set_exact_form): 'default' (sparse blocks 1 and K with the cached
+        primal aggregates), 'all_dual' (every edge tile carries a tangent) or 'sparse' (no cache)."""
+        forms = {"default": _lib.EXACT_FORM_DEFAULT, "all_dual": _lib.EXACT_FORM_ALL_DUAL,
+                 "sparse": _lib.EXACT_FORM_SPARSE}
+        _lib.check(self.lib.ecnf_set_exact_form(self._h, forms[form]))
 
     def base_sample(self, z) -> torch.Tensor:
         z = self._f32(z, (self.cfg.event_dim,), "z")

@@ -13,6 +13,7 @@ from __future__ import annotations
 import ctypes
 from typing import Optional
 
+import numpy as np
 import torch
 
 from . import _lib
@@ -54,7 +55,8 @@ def lj_log_prob(x: torch.Tensor, n_nodes: int = 13, dim: int = 3, epsilon: float
                 r=1.0, harmonic_potential_coef: float = 0.5) -> torch.Tensor:
     """leonard_jones.log_prob_fn: -energy(x) for x [..., n_nodes*dim] or [..., n_nodes, dim]; r is a float or a
     per-node array [n_nodes] (leonard_jones.py:10-20: pair (receiver i, sender j) uses r[i])."""
-    scalar = isinstance(r, (int, float))
+    # a Python / numpy scalar or a 0-d array / tensor is the scalar r; anything with n_nodes entries is per node
+    scalar = (torch.as_tensor(r).dim() == 0) if torch.is_tensor(r) else np.ndim(r) == 0
     t = _target(_lib.TARGET_LJ, n_nodes, dim, epsilon=epsilon, tau=tau, r=float(r) if scalar else 1.0,
                 harmonic_potential_coef=harmonic_potential_coef)
     return _log_prob(t, x, None if scalar else r)

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define ECNF_ABI_VERSION 2
+#define ECNF_ABI_VERSION 3
 
 enum ecnf_status {
   ECNF_OK = 0,
@@ -123,6 +123,30 @@ int ecnf_vf_jvp(ecnf_handle* h, const float* x, const float* t, const int32_t* f
 int ecnf_integrate(ecnf_handle* h, const ecnf_solve_opts* opts, const float* y0, const int32_t* feat,
                    const float* eps, float* y1, float* dlogp, int32_t* nfe, int32_t* status, int32_t batch,
                    void* stream);
+
+/* Device workspace of a solve.  The exact trace (ECNF_DIV_EXACT) runs N*D - D JVP passes per evaluation whose
+ * primal is the same; with a workspace, the first pass caches the primal edge aggregates of the blocks whose edge
+ * tangents are sparse (blocks 1 and K) and the later passes skip those primal tiles.  Results are bitwise equal with
+ * and without a workspace; only the time differs (LJ13 B = 1024 Euler-100 log_prob: ~1.35 s vs ~1.75 s).
+ *   ecnf_integrate_workspace_size  bytes a call with these options and batch needs (0: none is used)
+ *   ecnf_integrate_ws              ecnf_integrate with a CALLER-owned device workspace (NULL: none); the workspace is
+ *                                  used stream-ordered on `stream` only, so concurrent calls with distinct
+ *                                  workspaces are independent.  A non-NULL workspace below the size is ECNF_E_INVALID.
+ *   ecnf_reserve_workspace         allocate (synchronously, outside the solve calls) a handle-owned arena that
+ *                                  ecnf_integrate uses when it is large enough; calls on different streams that share
+ *                                  it are ordered by an event (no host synchronisation).
+ * The solve calls themselves never allocate or free device memory. */
+int ecnf_integrate_workspace_size(ecnf_handle* h, const ecnf_solve_opts* opts, int32_t batch, size_t* bytes);
+int ecnf_integrate_ws(ecnf_handle* h, const ecnf_solve_opts* opts, const float* y0, const int32_t* feat,
+                      const float* eps, float* y1, float* dlogp, int32_t* nfe, int32_t* status, int32_t batch,
+                      void* workspace, size_t workspace_bytes, void* stream);
+int ecnf_reserve_workspace(ecnf_handle* h, size_t bytes);
+
+/* A/B diagnostics of the exact trace (not needed in production; results: SPARSE and DEFAULT are bitwise equal, ALL_DUAL
+ * agrees to fp32 rounding):  DEFAULT  sparse blocks 1 and K + the primal cache when a workspace is available;
+ * ALL_DUAL every edge tile carries a tangent;  SPARSE  sparse blocks without the cache. */
+enum ecnf_exact_form { ECNF_EXACT_FORM_DEFAULT = 0, ECNF_EXACT_FORM_ALL_DUAL = 1, ECNF_EXACT_FORM_SPARSE = 2 };
+int ecnf_set_exact_form(ecnf_handle* h, int32_t form);
 
 /* x0 = base_scale * (z - mean_nodes(z)) for a standard-normal draw z [batch, N*D]. */
 int ecnf_base_sample(ecnf_handle* h, const float* z, float* x0, int32_t batch, void* stream);
@@ -207,6 +231,12 @@ int ecnf_adam_update(ecnf_trainer* tr, const float* grad, float* params, float* 
 
 /* Replace a handle's weights with the blob `params` (on_device: a DEVICE pointer, else host).  Synchronous. */
 int ecnf_update_params(ecnf_handle* h, const float* params, int32_t on_device);
+
+/* Layout of the ABI structs as this library was compiled: out[0] = sizeof, out[1 + i] = offsetof field i (declaration
+ * order) for which = 0 ecnf_cfg, 1 ecnf_solve_opts, 2 ecnf_target, 3 ecnf_adam_opts.  Writes min(cap, 1 + fields)
+ * values and returns the number of fields (-1 for an unknown `which`).  Bindings (ctypes, cgo, ...) check their struct
+ * mirrors against it. */
+int ecnf_struct_layout(int32_t which, size_t* out, int32_t cap);
 
 /* Thread-local description of the last error ("" when none). */
 const char* ecnf_last_error(void);

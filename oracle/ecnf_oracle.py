@@ -21,6 +21,9 @@ What it restates (all paths relative to the reference snapshot, Kalyan0821/ecnf-
 * ``ecnf/cnf/core.py:35-39``             optimal_transport_conditional_vf -> :func:`ot_conditional_vf`
 * ``ecnf/targets/target_energy/leonard_jones.py:10-35`` / ``double_well.py:9-28`` -> :func:`lj_energy`, :func:`dw_energy`
 * ``ecnf/utils/evaluation.py:10-22``, ``ecnf/setup_training.py:182``  -> :func:`forward_ess`, :func:`reverse_ess`
+* ``ecnf/utils/evaluation.py:25-115``, ``ecnf/setup_training.py:190-215``, ``ecnf/utils/numerical.py:43-52``
+                                          -> :func:`setup_padded_reshaped_data`, :func:`eval_test_set`,
+                                             :func:`maybe_masked_mean`
 
 Third-party arithmetic restated from its published algorithm (none of these packages is importable
 here and ``requirements.txt:1-16`` pins no versions):
@@ -675,3 +678,60 @@ def reverse_ess(log_w):
     """setup_training.py:182: 1 / sum(softmax(log_w)^2) / n."""
     log_w = np.asarray(log_w, np.float64)
     return float(np.exp(2 * _logsumexp(log_w) - _logsumexp(2 * log_w)) / log_w.size)
+
+
+# ----------------------------------------------------------------------------------------------
+# the test-set evaluation leg (SURVEY.md section 8f rank 2): evaluation.py:25-115, setup_training.py:190-215
+# ----------------------------------------------------------------------------------------------
+def setup_padded_reshaped_data(data, interval_length, reshape_axis=0):
+    """evaluation.py:25-50: pad the leading axis with zeros to a multiple of interval_length and reshape;
+    returns (reshaped data, mask) with mask 1 on the real rows."""
+    data = np.asarray(data)
+    n = data.shape[0]
+    pad = (interval_length - n % interval_length) % interval_length
+    padded = np.concatenate([data, np.zeros((pad,) + data.shape[1:], data.dtype)], axis=0)
+    mask = np.zeros(n + pad, dtype=int)
+    mask[:n] = 1
+    npad = n + pad
+    if reshape_axis == 0:
+        shape = (interval_length, npad // interval_length)
+    else:
+        assert reshape_axis == 1
+        shape = (npad // interval_length, interval_length)
+    return padded.reshape(shape + data.shape[1:]), mask.reshape(shape)
+
+
+def maybe_masked_mean(array, mask=None):
+    """numerical.py:43-52."""
+    array = np.asarray(array, np.float64)
+    if mask is None:
+        return float(array.mean())
+    mask = np.asarray(mask, np.float64)
+    divisor = mask.sum()
+    return float(np.where(mask > 0, array, 0.0).sum() * (0.0 if divisor == 0 else 1.0 / divisor))
+
+
+def eval_test_set(params, cfg, x, feat, batch_size, eps=None, approx=False, solver="euler", dt0=0.05,
+                  dtype=np.float64, target_log_prob=None):
+    """eval_fn (evaluation.py:59-115) with eval_on_data_batch_fn (setup_training.py:190-215) and, with a target,
+    calculate_forward_ess on the flattened log_w and mask (setup_training.py:239-241).  Per padded batch:
+    get_log_prob of every molecule (vmap), masked means of log_q / log_prob_base / delta; the batches' infos are
+    weighted by their share of the real rows (evaluation.py:92-97).  Padded rows never enter a mean (their values are
+    replaced by 0 under the mask), so only the real rows are solved here.  eps: [n, N*D] Hutchinson probes of the
+    real rows (approx=True)."""
+    x = np.asarray(x, np.float32)
+    n = x.shape[0]
+    xb, mask = setup_padded_reshaped_data(x, batch_size, reshape_axis=1)
+    lp, lp0, dl, _, _ = get_log_prob(params, cfg, x, feat, eps=eps, approx=approx, solver=solver, dt0=dt0,
+                                     dtype=dtype)
+    pad = xb.shape[0] * batch_size - n
+    full = lambda a: np.concatenate([np.asarray(a, np.float64), np.zeros(pad)]).reshape(mask.shape)
+    lq_b, lp0_b, dl_b = full(lp), full(lp0), full(dl)
+    w = mask.sum(-1) / mask.sum()
+    info = {"test_log_lik": float(sum(w[b] * maybe_masked_mean(lq_b[b], mask[b]) for b in range(len(w)))),
+            "test_log_prob_base": float(sum(w[b] * maybe_masked_mean(lp0_b[b], mask[b]) for b in range(len(w)))),
+            "test_delta_log_lik": float(sum(w[b] * maybe_masked_mean(dl_b[b], mask[b]) for b in range(len(w))))}
+    if target_log_prob is not None:
+        log_w = full(np.asarray(target_log_prob(x), np.float64) - np.asarray(lp, np.float64))
+        info["forward_ess"] = forward_ess(log_w.reshape(-1), mask.reshape(-1))
+    return info

@@ -1,7 +1,8 @@
 """Generate tests/golden/golden_v1.npz: inputs and fp64 oracle outputs for small cases of every config.
 
 The reference cannot run in this container (JAX absent) and ships no golden vectors, so these
-fixtures are the oracle's fp64 outputs (pinned by the KATs in tests/test_oracle.py).  They let the GPU parity tests
+fixtures are the oracle's fp64 outputs (and, for the log-densities, its fp32 outputs: the fp32-class bound of
+tests/tolerance.py) (pinned by the KATs in tests/test_oracle.py).  They let the GPU parity tests
 check the kernels without re-running the slow oracle, and let the CPU suite detect oracle drift.
 
 Params are NOT stored (LJ13 is 2 MB): they are regenerated from (config, seed) by oracle.init_params +
@@ -60,16 +61,25 @@ def main():
             x1, lq, _ = O.sample_and_log_prob(p, oc, x0, feat, eps=z, approx=True, solver="dopri5", dt0=0.1,
                                               dtype=np.float64)
             out[pre + "hutch_x1"], out[pre + "hutch_logq"] = x1, lq
+            x1, lq, _ = O.sample_and_log_prob(p, oc, x0, feat, eps=z, approx=True, solver="dopri5", dt0=0.1,
+                                              dtype=np.float32)
+            out[pre + "hutch_x1_f32"], out[pre + "hutch_logq_f32"] = x1, lq
         if name == "aldp":
             eps = rng.standard_normal(x0.shape).astype(np.float32)
             out[pre + "eps"] = eps
             lp, lp0, dl, _, xb = O.get_log_prob(p, oc, x0, feat, eps=eps, approx=True, solver="dopri5", dt0=0.1,
                                                dtype=np.float64)
             out[pre + "logp_hutch"], out[pre + "logp_hutch_dl"], out[pre + "logp_hutch_x0"] = lp, dl, xb
+            lp, lp0, dl, _, xb = O.get_log_prob(p, oc, x0, feat, eps=eps, approx=True, solver="dopri5", dt0=0.1,
+                                               dtype=np.float32)
+            out[pre + "logp_hutch_f32"], out[pre + "logp_hutch_dl_f32"] = lp, dl
         if name == "dw4":
             lp, lp0, dl, _, xb = O.get_log_prob(p, oc, x0, feat, approx=False, solver="dopri5", dt0=0.1,
                                                dtype=np.float64)
             out[pre + "logp_exact"], out[pre + "logp_exact_dl"], out[pre + "logp_exact_x0"] = lp, dl, xb
+            lp, lp0, dl, _, xb = O.get_log_prob(p, oc, x0, feat, approx=False, solver="dopri5", dt0=0.1,
+                                               dtype=np.float32)
+            out[pre + "logp_exact_f32"], out[pre + "logp_exact_dl_f32"] = lp, dl
     np.savez_compressed(OUT, **out)
     print(OUT, os.path.getsize(OUT), "bytes,", len(out), "arrays")
 

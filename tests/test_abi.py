@@ -38,7 +38,36 @@ def test_exports_every_declared_symbol(lib):
     nm = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True).stdout
     exported = set(re.findall(r"\bT (ecnf_\w+)", nm))
     assert declared <= exported, declared - exported
-    assert lib.ecnf_abi_version() == 2
+    assert lib.ecnf_abi_version() == 3
+
+
+def _ctypes_layout(cls):
+    return ctypes.sizeof(cls), [getattr(cls, f).offset for f, _ in cls._fields_]
+
+
+def test_struct_layouts_match_the_library(lib):
+    """The ctypes mirrors in ecnf_amd/_lib.py have the compiled library's sizeof and field offsets."""
+    for which, cls in enumerate(_lib.ABI_STRUCTS):
+        assert _ctypes_layout(cls) == _lib.struct_layout(which), cls.__name__
+    assert lib.ecnf_struct_layout(7, None, 0) == -1
+
+
+def test_integration_md_stub_matches_the_library(lib):
+    """Every ctypes.Structure in INTEGRATION.md's code blocks (the reference-side binding a maintainer would paste)
+    is executed and compared with the library's layout of the struct it mirrors (matched by its `# ecnf_*` comment)."""
+    text = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    blocks = re.findall(r"```python\n(.*?)```", text, re.S)
+    src = "\n".join(blocks)
+    structs = re.findall(r"^(class (\w+)\(ctypes\.Structure\):\s*# (ecnf_\w+)\n(?:[ \t]+.*\n)+)", src, re.M)
+    names = {c_name: (py_name, body) for body, py_name, c_name in structs}
+    which = {"ecnf_cfg": 0, "ecnf_solve_opts": 1, "ecnf_target": 2, "ecnf_adam_opts": 3}
+    assert set(names) == set(which), sorted(names)
+    for c_name, (py_name, body) in names.items():
+        ns = {"ctypes": ctypes}
+        exec(body, ns)
+        assert _ctypes_layout(ns[py_name]) == _lib.struct_layout(which[c_name]), c_name
+        # field names as in include/ecnf.h (and _lib.py)
+        assert [f for f, _ in ns[py_name]._fields_] == [f for f, _ in _lib.ABI_STRUCTS[which[c_name]]._fields_]
 
 
 @pytest.mark.parametrize("name", list(CONFIGS))
@@ -90,6 +119,12 @@ def test_create_without_gpu_fails_cleanly(lib):
 def test_null_handle_rejected(lib):
     assert lib.ecnf_vector_field(None, None, None, None, None, 1, None) == _lib.ECNF_E_INVALID
     assert lib.ecnf_integrate(None, None, None, None, None, None, None, None, None, 1, None) == _lib.ECNF_E_INVALID
+    assert lib.ecnf_integrate_ws(None, None, None, None, None, None, None, None, None, 1, None, 0,
+                                 None) == _lib.ECNF_E_INVALID
+    n = ctypes.c_size_t()
+    assert lib.ecnf_integrate_workspace_size(None, None, 1, ctypes.byref(n)) == _lib.ECNF_E_INVALID
+    assert lib.ecnf_reserve_workspace(None, 16) == _lib.ECNF_E_INVALID
+    assert lib.ecnf_set_exact_form(None, 0) == _lib.ECNF_E_INVALID
 
 
 def test_product_path_has_no_fallback():
@@ -100,8 +135,11 @@ def test_product_path_has_no_fallback():
         ROOT, "ecnf-baseline-neurips-2023_amd")
     out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
     assert "RAISED" in out.stdout, out.stderr
-    src = open(os.path.join(ROOT, "ecnf-baseline-neurips-2023_amd", "ecnf_amd", "engine.py")).read()
-    assert "oracle" not in src
+    pkg = os.path.join(ROOT, "ecnf-baseline-neurips-2023_amd", "ecnf_amd")
+    for f in sorted(os.listdir(pkg)):
+        if f.endswith(".py"):
+            src = open(os.path.join(pkg, f)).read()
+            assert "import oracle" not in src and "from oracle" not in src, f"{f} imports the oracle"
 
 
 def test_flatten_roundtrip_and_shape_errors():

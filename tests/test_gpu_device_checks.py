@@ -3,7 +3,8 @@
 tools/debug/build.sh compiles the LJ13-shape kernels with ECNF_DCHECK bounds checks (egnn_eval.hpp: LDS carve-up
 against the launch's dynamic LDS, edge receiver / sender rows, edge tiles, node-GEMM row tiles, stored segment
 parts, molecule slots).  A child process runs every LJ13 mode through that library at batch sizes that exercise the
-batch-aware workgroup sizing (1, 5, 13, 300, 1024 molecules) and reads the failed-check bits with
+batch-aware workgroup sizing (1, 5, 13, 300, 1024 molecules; the exact trace at every size, so the bounds of its
+primal-aggregate cache slots are checked at 1024 molecules too, bit 6) and reads the failed-check bits with
 ecnf_debug_checks(); they must be 0, and the outputs must match the product library (the checks do not touch the
 arithmetic)."""
 import json
@@ -45,10 +46,9 @@ for B in (1, 5, 13, 300, 1024):
     y, _, _, _ = h.integrate(x0, feat, 0.0, 1.0, SolveOptions("euler", 0.1))
     yh, dl, _, _ = h.integrate(x0, feat, 0.0, 1.0, SolveOptions("euler", 0.25), _lib.DIV_HUTCHINSON, z)
     ya, _, nfe, _ = h.integrate(x0, feat, 0.0, 1.0, SolveOptions("dopri5", None))
-    rec = dict(z=z, v=v, ju=ju, y=y, yh=yh, dl=dl, ya=ya)
-    if B <= 5:
-        ye, dle, _, _ = h.integrate(x0, feat, 1.0, 0.0, SolveOptions("euler", 0.5), _lib.DIV_EXACT)
-        rec.update(ye=ye, dle=dle)
+    # the exact trace with its primal-aggregate cache in a caller workspace (every cache slot of the grid touched)
+    ye, dle, _, _ = h.integrate(x0, feat, 1.0, 0.0, SolveOptions("euler", 0.5), _lib.DIV_EXACT)
+    rec = dict(z=z, v=v, ju=ju, y=y, yh=yh, dl=dl, ya=ya, ye=ye, dle=dle)
     out[B] = {k: w.detach().cpu().numpy() for k, w in rec.items()}
 lib.ecnf_debug_checks(ctypes.byref(flags), 1)
 np.savez(sys.argv[1], **{f"{B}_{k}": w for B, d in out.items() for k, w in d.items()})
@@ -83,7 +83,8 @@ def test_device_checks_pass_and_match_product(tmp_path):
         y, _, _, _ = h.integrate(x0, feat, 0.0, 1.0, SolveOptions("euler", 0.1))
         v = h.vector_field(x0, t, feat)
         yh, dl, _, _ = h.integrate(x0, feat, 0.0, 1.0, SolveOptions("euler", 0.25), _lib.DIV_HUTCHINSON, z)
-        for name, got in (("y", y), ("v", v), ("yh", yh), ("dl", dl)):
+        ye, dle, _, _ = h.integrate(x0, feat, 1.0, 0.0, SolveOptions("euler", 0.5), _lib.DIV_EXACT)
+        for name, got in (("y", y), ("v", v), ("yh", yh), ("dl", dl), ("ye", ye), ("dle", dle)):
             ref = C[f"{B}_{name}"]
             err = np.abs(got.cpu().numpy() - ref).max() / max(1.0, np.abs(ref).max())
             assert err <= 1e-6, (B, name, err)

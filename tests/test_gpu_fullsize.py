@@ -6,6 +6,12 @@ of it are checked against the fp64 oracle and bitwise against a small-batch run 
     get_log_prob with PIDController(rtol = atol = 1e-5) and Hutchinson: 4 strided molecules held to the adaptive
     envelope of test_gpu_parity.py (within 2x (+2e-4 / +2e-3) the largest distance of the fp32 oracle's own solves
     of x and 3 perturbed copies to an accurate fp64 fixed-step solution)
+  * LJ13, B = 1024, get_log_prob(approx=False) with Euler NFE = 100: the shipped exact trace (sparse blocks 1 and K,
+    primal aggregates cached in a caller workspace of 1024 + MPW slots) for the whole batch in one launch; 3 strided
+    molecules fp32-class (tests/tolerance.py) in x and the log-density against the fp64 / fp32 oracle's full N*D trace,
+    and bitwise against a small-batch run of the same molecules (other workgroup sizes, other cache slots)
+  * ALDP, B = 512 real frames, get_log_prob(approx=False) with Euler NFE = 20: the same checks on 2 strided molecules
+    (ALDP: 15 primal + 2 dual tiles per molecule in the sparse blocks)
   * QM9 shape (N = 29, M = 256, L = 4, K = 5), B = 2048, Euler NFE = 10 (the full NFE-100 batch is timed by
     tools/bench_paths.py; 10 steps bound the oracle's CPU time): 2 strided molecules vs fp64, |err| <= 1e-4
 """
@@ -16,6 +22,7 @@ import pytest
 import torch
 
 from oracle import ecnf_oracle as O
+from tolerance import fp32_class
 
 pytestmark = pytest.mark.gpu
 
@@ -57,12 +64,50 @@ def test_lj13_b1024_euler100():
     assert torch.equal(y[idx], y_small)
 
 
+def _aldp_frames(B):
+    frames = np.load(os.path.join(HERE, "golden", "aldp_frames.npy")).astype(np.float32)
+    assert frames.shape[0] >= B and frames.shape[1:] == (22, 3)
+    frames = frames[:B]
+    return (frames - frames.mean(axis=1, keepdims=True)).reshape(B, -1)   # setup_training.py:91-94
+
+
+def _exact_fullsize(name, x, feat, p, oc, h, dt, idx):
+    xb, dl, nfe, st = h.integrate(g(x), g(feat, torch.int32), 1.0, 0.0, SolveOptions("euler", dt),
+                                  divergence=_lib.DIV_EXACT)
+    assert (st.cpu().numpy() == 0).all() and torch.isfinite(dl).all()
+    assert (nfe.cpu().numpy() == round(1 / dt)).all()
+    lp = h.base_log_prob(xb) + dl
+    r64 = O.get_log_prob(p, oc, x[idx], feat[idx], approx=False, solver="euler", dt0=dt, dtype=np.float64)
+    r32 = O.get_log_prob(p, oc, x[idx], feat[idx], approx=False, solver="euler", dt0=dt, dtype=np.float32)
+    fp32_class(f"{name} exact x", xb[idx], r64[4], r32[4])
+    fp32_class(f"{name} exact dl", dl[idx], r64[2], r32[2])
+    fp32_class(f"{name} exact log_p", lp[idx], r64[0], r32[0])
+    xs, dls, _, _ = h.integrate(g(x[idx]), g(feat[idx], torch.int32), 1.0, 0.0, SolveOptions("euler", dt),
+                                divergence=_lib.DIV_EXACT)
+    assert torch.equal(xb[idx], xs) and torch.equal(dl[idx], dls)
+
+
+@pytest.mark.timeout(400)
+def test_lj13_b1024_exact_log_prob_euler100():
+    """get_log_prob(approx=False) (sample_and_log_prob.py:57-67) at the headline batch and NFE."""
+    cfg, oc, p, z, h = _setup("lj13", 1024)
+    x = O.base_sample(z, oc)
+    feat = np.zeros((1024, cfg.n_nodes), np.int32)
+    _exact_fullsize("lj13 B=1024", x, feat, p, oc, h, 0.01, np.array([0, 511, 1023]))
+
+
+@pytest.mark.timeout(300)
+def test_aldp_b512_exact_log_prob_real_frames():
+    cfg, oc, p, _, h = _setup("aldp", 512)
+    x = _aldp_frames(512)
+    feat = np.tile(np.arange(22, dtype=np.int32), (512, 1))          # data.py:146
+    _exact_fullsize("aldp B=512", x, feat, p, oc, h, 0.05, np.array([0, 511]))
+
+
 @pytest.mark.timeout(400)
 def test_aldp_b512_adaptive_hutchinson_log_prob():
     cfg, oc, p, _, h = _setup("aldp", 512)
-    frames = np.load(os.path.join(HERE, "golden", "aldp_frames.npy")).astype(np.float32)
-    assert frames.shape == (512, 22, 3)
-    x = (frames - frames.mean(axis=1, keepdims=True)).reshape(512, -1)
+    x = _aldp_frames(512)
     feat = np.tile(np.arange(22, dtype=np.int32), (512, 1))          # data.py:146
     eps = np.random.default_rng(4321).standard_normal(x.shape).astype(np.float32)
     xb, dl, nfe, st = h.integrate(g(x), g(feat, torch.int32), 1.0, 0.0, SolveOptions("dopri5", None),
@@ -85,8 +130,10 @@ def test_aldp_b512_adaptive_hutchinson_log_prob():
         if k == 0:
             nfe_32 = nfe_k
     ek = np.abs(xb.cpu().numpy()[idx] - x_f).max()
+    print(f"aldp adaptive x: kernel {ek:.3e}, oracle envelope {eo_x:.3e}")
     assert ek <= 2 * eo_x + 2e-4, (ek, eo_x)
     ek = np.abs(lp[idx] - lp_f).max()
+    print(f"aldp adaptive log_p: kernel {ek:.3e}, oracle envelope {eo_lp:.3e}")
     assert ek <= 2 * eo_lp + 2e-3, (ek, eo_lp)
     nfe = nfe.cpu().numpy()
     assert abs(nfe[idx].mean() - nfe_32.mean()) <= 0.3 * nfe_32.mean(), (nfe[idx], nfe_32)

@@ -23,7 +23,7 @@ if not torch.cuda.is_available():
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ARGS = ["--batch", "96", "--nfe", "10", "--steps", "1", "--warmup", "1", "--logprob", "1", "--fp32-steps", "0", "--train-steps", "0",
-        "--cpu-molecules", "0"]
+        "--cpu-molecules", "0", "--pmc", "0"]
 
 
 def _run(gpus, dump, backend="gloo"):
@@ -54,10 +54,9 @@ def test_two_ranks_match_one_rank(tmp_path):
         cat = np.concatenate([p[key] for p in parts])
         assert np.array_equal(cat, r1[key]), key
     log_w = r1["log_w"].astype(np.float64)
-    rev, fwd = O.reverse_ess(log_w), O.forward_ess(log_w)
+    rev = O.reverse_ess(log_w)
     for res in (one, two):
         lp = res["logprob"]
         assert lp["status_ok"]
         assert abs(lp["rev_ess"] - rev) <= 1e-5 * rev + 1e-9, (lp["rev_ess"], rev)
-        assert abs(lp["fwd_ess"] - fwd) <= 1e-5 * max(fwd, 1e-6) + 1e-9, (lp["fwd_ess"], fwd)
         assert abs(lp["mean_log_q"] - float(r1["log_q"].astype(np.float64).mean())) <= 1e-4

@@ -6,15 +6,16 @@ Tolerances (fp32 kernel vs fp64 oracle; stated per test):
   * adaptive Dopri5: step sequences fork in fp32, so the kernel must be within 2x the largest distance of the
     oracle's own fp32 adaptive solves (x0 and 1e-7-perturbed copies) to an accurate fp64 fixed-step solution,
     batch-mean NFE within 30 % of the oracle's
-  * log-densities: |err| <= 2e-3 absolute (values are O(10-100))
+  * log-densities of fixed-step solves: fp32-class (tests/tolerance.py: |hip - fp64| <= 4 |fp32 oracle - fp64| +
+    2e-7 max(1, |fp64|)), the same bound the precision contract puts on positions
 """
-import os
 
 import numpy as np
 import pytest
 import torch
 
 from oracle import ecnf_oracle as O
+from tolerance import fp32_class
 
 pytestmark = pytest.mark.gpu
 
@@ -226,17 +227,12 @@ def test_log_prob_exact_fixed():
     oc, params, h, z, x0, feat = setup(cfg, B=5)
     x, dl, nfe, _ = h.integrate(g(x0), g(feat, torch.int32), 1.0, 0.0, SolveOptions("dopri5", 0.05),
                                 divergence=_lib.DIV_EXACT)
-    lp_ref, lp0_ref, dl_ref, nfe_ref, x_ref = O.get_log_prob(params, oc, x0, feat, approx=False, solver="dopri5",
-                                                             dt0=0.05, dtype=np.float64)
-    assert np.abs(x.cpu().numpy() - x_ref).max() <= 1e-4
-    assert np.abs(dl.cpu().numpy() - dl_ref).max() <= 2e-3
+    r64 = O.get_log_prob(params, oc, x0, feat, approx=False, solver="dopri5", dt0=0.05, dtype=np.float64)
+    r32 = O.get_log_prob(params, oc, x0, feat, approx=False, solver="dopri5", dt0=0.05, dtype=np.float32)
+    fp32_class("tiny exact x", x, r64[4], r32[4])
+    fp32_class("tiny exact dl", dl, r64[2], r32[2])
     lp = h.base_log_prob(x) + dl
-    assert np.abs(lp.cpu().numpy() - lp_ref).max() <= 2e-3
-
-
-def _exact_env(sparse, pcache):
-    os.environ["ECNF_EXACT_SPARSE"] = sparse
-    os.environ["ECNF_EXACT_PCACHE"] = pcache
+    fp32_class("tiny exact log_p", lp, r64[0], r32[0])
 
 
 @pytest.mark.parametrize("name,B,dt", [("lj13", 3, 1.0), ("aldp", 2, 1.0), ("lj13", 3, 0.05), ("aldp", 2, 0.1)])
@@ -244,36 +240,92 @@ def test_log_prob_exact_sparse_block1(name, B, dt):
     """Exact trace where blocks 1 and K run every edge as a primal tile and only 2(N-1) edges as dual tiles
     (egnn_eval sparse_a; block 1: the edges at the unit tangent's atom a, block K: the edges into atoms 0 and a, the
     two JVP components the trace reads; LJ13: 5 primal + 1 dual tile per molecule, ALDP 15 + 2), and where the
-    primal aggregates of those blocks are cached over the ND - D JVP passes of an evaluation (SolveP::pcache): vs
-    the all-dual form of the same kernel (ECNF_EXACT_SPARSE=0), the sparse form without the cache
-    (ECNF_EXACT_PCACHE=0), and the fp64 oracle's full N*D trace."""
+    primal aggregates of those blocks are cached over the ND - D JVP passes of an evaluation (SolveP::pcache, the
+    shipped default with a workspace): vs the all-dual form of the same kernel and the sparse form without the cache
+    (ecnf_set_exact_form, A/B diagnostics), and the fp64 / fp32 oracle's full N*D trace."""
     cfg = CONFIGS[name]
     oc, params, h, z, x0, feat = setup(cfg, B=B)
     opts = SolveOptions("euler", dt)
     out = {}
     try:
-        for form, env in (("dense", ("0", "1")), ("sparse", ("1", "0")), ("cached", ("1", "1"))):
-            _exact_env(*env)
+        for form in ("all_dual", "sparse", "default"):
+            h.set_exact_form(form)
             x, dl, _, st = h.integrate(g(x0), g(feat, torch.int32), 1.0, 0.0, opts, divergence=_lib.DIV_EXACT)
             assert (st.cpu().numpy() == 0).all()
             out[form] = (x, dl)
     finally:
-        del os.environ["ECNF_EXACT_SPARSE"], os.environ["ECNF_EXACT_PCACHE"]
-    _, _, dl_ref, _, x_ref = O.get_log_prob(params, oc, x0, feat, approx=False, solver="euler", dt0=dt,
-                                            dtype=np.float64)
-    x, dl = out["cached"]
-    ox, odl = np.abs(x.cpu().numpy() - x_ref).max(), np.abs(dl.cpu().numpy() - dl_ref).max()
-    print(f"{name} dt={dt}: vs fp64 |dx| {ox:.3g} |ddl| {odl:.3g}")
-    assert ox <= 1e-4 and odl <= 2e-3, (ox, odl)
+        h.set_exact_form("default")
+    r64 = O.get_log_prob(params, oc, x0, feat, approx=False, solver="euler", dt0=dt, dtype=np.float64)
+    r32 = O.get_log_prob(params, oc, x0, feat, approx=False, solver="euler", dt0=dt, dtype=np.float32)
+    x, dl = out["default"]
+    fp32_class(f"{name} dt={dt} exact x", x, r64[4], r32[4])
+    fp32_class(f"{name} dt={dt} exact dl", dl, r64[2], r32[2])
     # the skipped edge tangents are exact zeros and the cached aggregates are the recomputed ones: the forms differ
-    # at most by rounding (receiver a's block-1 segment sum runs over different lanes)
-    xd, dld = out["dense"]
-    for form in ("sparse", "cached"):
+    # from the all-dual form at most by rounding (receiver a's block-1 segment sum runs over different lanes), and
+    # the cached form is bitwise the uncached sparse form
+    xd, dld = out["all_dual"]
+    for form in ("sparse", "default"):
         xf, dlf = out[form]
         ex, edl = float((xf - xd).abs().max()), float((dlf - dld).abs().max())
-        print(f"{name} dt={dt}: {form} vs dense |dx| {ex:.3g} |ddl| {edl:.3g}")
+        print(f"{name} dt={dt}: {form} vs all_dual |dx| {ex:.3g} |ddl| {edl:.3g}")
         assert ex <= 1e-5 and edl <= 1e-4 * max(1.0, float(dld.abs().max())), (form, ex, edl)
-    assert torch.equal(out["sparse"][0], out["cached"][0]) and torch.equal(out["sparse"][1], out["cached"][1])
+    assert torch.equal(out["sparse"][0], out["default"][0]) and torch.equal(out["sparse"][1], out["default"][1])
+
+
+def test_exact_workspace_forms_and_streams():
+    """The exact trace's workspace contract (include/ecnf.h ecnf_integrate_ws): no workspace, a caller workspace
+    and the handle arena (ecnf_reserve_workspace) give bitwise equal results; an undersized workspace is rejected;
+    two solves on two streams sharing the handle arena, with different inputs, each match their single-stream
+    result (the arena is ordered across streams by an event)."""
+    import ctypes
+    cfg = CONFIGS["lj13"]
+    oc, params, h, z, x0, feat = setup(cfg, B=40)
+    opts = SolveOptions("euler", 0.5)
+    fd = g(feat, torch.int32)
+    ref, dref, _, _ = h.integrate(g(x0), fd, 1.0, 0.0, opts, divergence=_lib.DIV_EXACT)     # caller workspace
+    o = opts.to_c(1.0, 0.0, _lib.DIV_EXACT)
+    nb = ctypes.c_size_t()
+    _lib.check(h.lib.ecnf_integrate_workspace_size(h._h, ctypes.byref(o), 40, ctypes.byref(nb)))
+    assert nb.value > 0
+    B = x0.shape[0]
+
+    def raw(x, ws=None, nbytes=0, arena=False, stream=None):
+        y1 = torch.empty_like(x)
+        dl = torch.empty(x.shape[0], device=DEV)
+        st = torch.empty(x.shape[0], device=DEV, dtype=torch.int32)
+        s = (stream or torch.cuda.current_stream()).cuda_stream
+        if arena:
+            rc = h.lib.ecnf_integrate(h._h, ctypes.byref(o), x.data_ptr(), fd.data_ptr(), None, y1.data_ptr(),
+                                      dl.data_ptr(), None, st.data_ptr(), x.shape[0], s)
+        else:
+            rc = h.lib.ecnf_integrate_ws(h._h, ctypes.byref(o), x.data_ptr(), fd.data_ptr(), None, y1.data_ptr(),
+                                         dl.data_ptr(), None, st.data_ptr(), x.shape[0],
+                                         None if ws is None else ws.data_ptr(), nbytes, s)
+        return rc, y1, dl, st
+
+    rc, y, dl, st = raw(g(x0))                                  # no workspace: the uncached sparse form
+    assert rc == 0 and torch.equal(y, ref) and torch.equal(dl, dref)
+    small = torch.empty(nb.value // 2, device=DEV, dtype=torch.uint8)
+    rc, _, _, _ = raw(g(x0), small, small.numel())
+    assert rc == _lib.ECNF_E_INVALID
+    _lib.check(h.lib.ecnf_reserve_workspace(h._h, 4 * nb.value))
+    rc, y, dl, st = raw(g(x0), arena=True)
+    assert rc == 0 and torch.equal(y, ref) and torch.equal(dl, dref)
+    # two streams, one arena, different inputs
+    x_b = g(x0[::-1].copy())
+    ref_b, dref_b, _, _ = h.integrate(x_b, fd, 1.0, 0.0, opts, divergence=_lib.DIV_EXACT)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    xa = g(x0)
+    torch.cuda.synchronize()
+    for _ in range(3):
+        with torch.cuda.stream(s1):
+            ra = raw(xa, arena=True, stream=s1)
+        with torch.cuda.stream(s2):
+            rb = raw(x_b, arena=True, stream=s2)
+        torch.cuda.synchronize()
+        assert ra[0] == 0 and rb[0] == 0
+        assert torch.equal(ra[1], ref) and torch.equal(ra[2], dref)
+        assert torch.equal(rb[1], ref_b) and torch.equal(rb[2], dref_b)
 
 
 def test_sample_and_log_prob_hutchinson_fixed():
@@ -284,9 +336,11 @@ def test_sample_and_log_prob_hutchinson_fixed():
                                  divergence=_lib.DIV_HUTCHINSON, eps=g(z))
     x1r, lq_ref, _ = O.sample_and_log_prob(params, oc, x0, feat, eps=z, approx=True, solver="dopri5", dt0=0.05,
                                            dtype=np.float64)
-    assert np.abs(x1.cpu().numpy() - x1r).max() <= 1e-4
+    x1r32, lq_32, _ = O.sample_and_log_prob(params, oc, x0, feat, eps=z, approx=True, solver="dopri5", dt0=0.05,
+                                            dtype=np.float32)
+    fp32_class("lj13 hutchinson x1", x1, x1r, x1r32)
     lq = (h.base_log_prob(g(x0)) - dl).cpu().numpy()
-    assert np.abs(lq - lq_ref).max() <= 2e-3
+    fp32_class("lj13 hutchinson log_q", lq, lq_ref, lq_32)
 
 
 def test_log_prob_adaptive_hutchinson():
@@ -302,6 +356,7 @@ def test_log_prob_adaptive_hutchinson():
     ek, eo = np.abs(x.cpu().numpy() - x_fine).max(), np.abs(x_ref - x_fine).max()
     assert ek <= 2 * eo + 2e-4, (ek, eo)
     ek, eo = np.abs(dl.cpu().numpy() - dl_fine).max(), np.abs(dl_ref - dl_fine).max()
+    print(f"aldp adaptive hutchinson dl: kernel {ek:.3e}, oracle {eo:.3e}")
     assert ek <= 2 * eo + 2e-3, (ek, eo)
 
 

@@ -170,3 +170,26 @@ def test_device_feature_ids_checked_in_kernel():
         h.integrate(g(x0), bad, 0.0, 1.0, SolveOptions("euler", 0.25))
     with pytest.raises(ValueError):     # host features: checked before the upload
         h.vector_field(g(x0), t, np.full((3, cfg.n_nodes), -1, np.int32))
+
+
+def test_huge_chain_weight_runs_strict_fp32():
+    """An edge-MLP weight >= 2^15 cannot be split into unscaled fp16 pieces: ecnf_create makes the handle strict
+    fp32 (instead of refusing it), the results are fp32-class, and asking for the split arithmetic is refused."""
+    cfg, oc, p, x0, feat = _inputs("lj13", 6, stress=False)
+    p = dict(p)
+    w = p["EGNN_0/1/phi_x_torso/Dense_1/kernel"].copy()
+    w[3, 5] = 40000.0
+    p["EGNN_0/1/phi_x_torso/Dense_1/kernel"] = w
+    h = EcnfHandle(cfg, p, 0)
+    assert h.precision == "fp32" and h.chain_arithmetic() == "fp32_mfma"
+    with pytest.raises(ValueError):
+        h.set_precision("split_f16")
+    t = np.linspace(0.1, 0.9, 6).astype(np.float32)
+    v = h.vector_field(g(x0), g(t), g(feat, torch.int32)).cpu().numpy()
+    ref64 = O.egnn_vector_field(p, oc, x0, t, feat, dtype=np.float64)
+    ref32 = O.egnn_vector_field(p, oc, x0, t, feat, dtype=np.float32)
+    _check("lj13 huge weight eval", v, ref64, ref32)
+    # back to ordinary weights: the split arithmetic is available again
+    h.update_params(O.init_params(oc, 0))
+    h.set_precision("split_f16")
+    assert h.chain_arithmetic() == "split_f16"

@@ -81,6 +81,11 @@ def test_lj13_per_node_r():
     assert err.max() <= 1e-5, err.max()
     with pytest.raises(ValueError):
         T.lj_log_prob(torch.from_numpy(x).cuda(), 13, 3, r=torch.ones(12, device="cuda"))
+    # scalar r given as a numpy scalar or a 0-d tensor: the scalar form, not a per-node array
+    xd = torch.from_numpy(x).cuda().reshape(257, -1)
+    ref = T.lj_log_prob(xd, 13, 3, r=1.1)
+    for r0 in (np.float32(1.1), np.array(1.1, np.float32), torch.tensor(1.1), torch.tensor(1.1, device="cuda")):
+        assert torch.equal(T.lj_log_prob(xd, 13, 3, r=r0), ref), type(r0)
 
 
 @pytest.mark.parametrize("n", [5, 3000])

@@ -85,6 +85,26 @@ def test_step_is_deterministic_and_batch_bounds():
                          np.concatenate([feat, feat]))
 
 
+def test_device_feature_ids_out_of_range():
+    """Device-resident features are not validated on the host (no sync): an out-of-range id must never index past the
+    embedding table; its molecule makes the loss and the gradient NaN instead of reading other params."""
+    cfg = CONFIGS["aldp"]
+    oc, p, x1, x0, t, feat = _case(cfg, 4)
+    tr = TR.Trainer(cfg, max_batch=4, device=0)
+    l_ok, g_ok = tr.loss_and_grad(p, x1, x0, t, torch.from_numpy(feat).cuda())
+    assert torch.isfinite(l_ok) and torch.isfinite(g_ok).all()
+    for bad_id in (cfg.n_features, -1, 1 << 30):
+        bad = torch.from_numpy(feat).cuda()
+        bad[2, 5] = bad_id
+        l_bad, g_bad = tr.loss_and_grad(p, x1, x0, t, bad)
+        assert torch.isnan(l_bad), bad_id
+        assert torch.isnan(g_bad).any(), bad_id
+    with pytest.raises(ValueError):     # host features: checked before the upload
+        f = feat.copy()
+        f[0, 0] = cfg.n_features
+        tr.loss_and_grad(p, x1, x0, t, f)
+
+
 def _adam_ref(g, p, mu, nu, lr, count, b1=0.9, b2=0.999, eps=1e-8):
     """optax.scale_by_adam + scale(-lr) + apply_updates (bias corrections with the incremented count)."""
     g, p, mu, nu = (np.asarray(a, np.float64) for a in (g, p, mu, nu))

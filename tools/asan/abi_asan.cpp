@@ -7,6 +7,9 @@
 // With a GPU it also runs each C-ABI entry point once on a small batch and the error paths that follow a valid
 // handle.  Exit status 0 = every check passed and ASan reported nothing (ASan aborts the process otherwise).
 #include <hip/hip_runtime.h>
+#include <sanitizer/lsan_interface.h>
+
+#include <chrono>
 
 #include <cmath>
 #include <cstdio>
@@ -141,6 +144,26 @@ static bool device_checks(const ecnf_cfg& c, int B) {
   CHECK(rcd == ECNF_E_INVALID, "hutchinson without eps: %d", rcd);
   rcd = ecnf_integrate(h, &o, x, feat, z, y, dl, nfe, st, B, nullptr);
   CHECK(rcd == ECNF_OK || rcd == ECNF_E_UNSUPPORTED, "hutchinson: %d", rcd);
+  // the exact trace: caller workspace (ecnf_integrate_ws), the handle arena, the A/B forms
+  o.divergence = ECNF_DIV_EXACT; o.t0 = 1.f; o.t1 = 0.f; o.dt0 = 0.5f;
+  size_t wsb = 0;
+  CHECK(ecnf_integrate_workspace_size(h, &o, B, &wsb) == ECNF_OK, "workspace size");
+  float* ws = wsb ? dev_alloc<float>(wsb / sizeof(float) + 1) : nullptr;
+  rcd = ecnf_integrate_ws(h, &o, x, feat, nullptr, y, dl, nfe, st, B, ws, wsb, nullptr);
+  CHECK(rcd == ECNF_OK || rcd == ECNF_E_UNSUPPORTED, "exact with workspace: %d", rcd);
+  if (wsb) {
+    CHECK(ecnf_integrate_ws(h, &o, x, feat, nullptr, y, dl, nfe, st, B, ws, wsb / 2, nullptr) == ECNF_E_INVALID,
+          "undersized workspace");
+    CHECK(ecnf_reserve_workspace(h, wsb) == ECNF_OK, "reserve workspace");
+  }
+  CHECK(ecnf_set_exact_form(h, ECNF_EXACT_FORM_SPARSE) == ECNF_OK, "exact form");
+  CHECK(ecnf_set_exact_form(h, 7) == ECNF_E_INVALID, "bad exact form");
+  rcd = ecnf_integrate(h, &o, x, feat, nullptr, y, dl, nfe, st, B, nullptr);
+  CHECK(rcd == ECNF_OK || rcd == ECNF_E_UNSUPPORTED, "exact (sparse form): %d", rcd);
+  CHECK(ecnf_set_exact_form(h, ECNF_EXACT_FORM_DEFAULT) == ECNF_OK, "exact form default");
+  rcd = ecnf_integrate(h, &o, x, feat, nullptr, y, dl, nfe, st, B, nullptr);
+  CHECK(rcd == ECNF_OK || rcd == ECNF_E_UNSUPPORTED, "exact (arena): %d", rcd);
+  o.t0 = 0.f; o.t1 = 1.f; o.dt0 = 0.1f; o.divergence = ECNF_DIV_HUTCHINSON;
   o.solver = 9;
   CHECK(ecnf_integrate(h, &o, x, feat, z, y, dl, nfe, st, B, nullptr) == ECNF_E_INVALID, "bad solver");
   CHECK(ecnf_set_precision(h, 5) == ECNF_E_INVALID, "bad precision");
@@ -173,8 +196,8 @@ static bool device_checks(const ecnf_cfg& c, int B) {
   }
   CHECK(ecnf_destroy(h) == ECNF_OK, "destroy");
   for (void* q : {(void*)z, (void*)x, (void*)v, (void*)y, (void*)tt, (void*)lp, (void*)dl, (void*)feat, (void*)nfe,
-                  (void*)st})
-    hipFree(q);
+                  (void*)st, (void*)ws})
+    if (q) hipFree(q);
   return true;
 }
 
@@ -187,6 +210,18 @@ int main() {
     if (g_trace) std::fprintf(stderr, "config N = %d, M = %d\n", c.n_nodes, c.mlp_width);
     gpu += device_checks(c, 5) ? 1 : 0;
   }
+  {
+    size_t lay[16];
+    for (int w = 0; w < 4; ++w) CHECK(ecnf_struct_layout(w, lay, 16) > 0, "struct layout %d", w);
+    CHECK(ecnf_struct_layout(9, lay, 16) == -1, "bad struct");
+  }
+  // scoped leak check of every allocation made through the library above (the ROCm runtime's own allocations are
+  // suppressed by lsan.supp); run here, while the process is live, instead of at exit (leak_check_at_exit=0)
+  const auto t0 = std::chrono::steady_clock::now();
+  const int leaked = __lsan_do_recoverable_leak_check();
+  const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  std::printf("abi_asan: leak check %s in %.0f ms\n", leaked ? "FOUND LEAKS" : "clean", ms);
+  if (leaked) ++g_fail;
   std::printf("abi_asan: %s, %d failure(s)\n", gpu ? "host + device paths" : "host paths only (no GPU)", g_fail);
   return g_fail ? 1 : 0;
 }
