@@ -26,7 +26,8 @@ import torch
 
 from . import _lib
 from .engine import EcnfHandle, SolveOptions
-from .params import CNFConfig, flatten_params, init_params
+from .params import (CNFConfig, flatten_params, init_from_spec, init_params, kernel_config, pad_params,
+                     ref_param_spec)
 
 Params = Union[Mapping, np.ndarray, EcnfHandle]
 
@@ -115,22 +116,32 @@ def _batched(features, cfg: CNFConfig, n: Optional[int]):
 def build_cnf(n_frames: int, dim: int, sigma_min: float, base_scale: float, n_blocks_egnn: int,
               mlp_units: Sequence[int], n_invariant_feat_hidden: int, time_embedding_dim: int, n_features: int,
               device: Union[int, str, torch.device] = 0) -> FlowMatchingCNF:
-    """build_cnf.py:34-102: zero-CoM scaled Gaussian base + FlatEgnn vector field (on the HIP engine)."""
+    """build_cnf.py:34-102: zero-CoM scaled Gaussian base + FlatEgnn vector field (on the HIP engine).
+
+    Any mlp_units (each <= 256, a compiled depth) and n_invariant_feat_hidden run on the compiled kernel shape
+    params.kernel_config picks: the reference-shaped params are zero-padded on upload (params.pad_params), which
+    leaves the function unchanged.  ``cfg`` is that kernel shape; ``init`` returns reference-shaped params."""
     units = tuple(int(u) for u in mlp_units)
-    if len(set(units)) != 1:
-        raise ValueError("the fused kernel needs equal mlp_units (the reference configs all use equal widths)")
-    cfg = CNFConfig(n_nodes=int(n_frames), dim=int(dim), n_features=int(n_features),
-                    hidden=int(n_invariant_feat_hidden), time_embedding_dim=int(time_embedding_dim),
-                    mlp_width=units[0], mlp_depth=len(units), n_blocks=int(n_blocks_egnn),
-                    base_scale=float(base_scale), sigma_min=float(sigma_min))
+    H = int(n_invariant_feat_hidden)
+    cfg = kernel_config(int(n_frames), int(dim), int(n_features), H, int(time_embedding_dim), units,
+                        int(n_blocks_egnn), float(base_scale), float(sigma_min))
+    padded = units != cfg.mlp_units or H != cfg.hidden
     dev = torch.device(device) if not isinstance(device, int) else torch.device("cuda", device)
 
     def init(key, x=None, t=None, features=None):
         seed = key if isinstance(key, (int, np.integer)) else 0
-        return init_params(cfg, int(seed))
+        if not padded:
+            return init_params(cfg, int(seed))
+        return init_from_spec(ref_param_spec(cfg.n_features, H, cfg.time_embedding_dim, units, cfg.n_blocks),
+                              int(seed))
+
+    def to_device(params):
+        if padded and not isinstance(params, (EcnfHandle, np.ndarray)):
+            params = pad_params(params, H, cfg.time_embedding_dim, units, cfg)
+        return device_params(params, cfg, dev)
 
     def apply(params, x, t, features=None):
-        h = device_params(params, cfg, dev)
+        h = to_device(params)
         x = torch.as_tensor(x, device=dev, dtype=torch.float32)
         if x.dim() != 2:
             raise ValueError("positions must be rank 2 [batch, n_frames*dim] (build_cnf.py:73)")
@@ -169,7 +180,7 @@ def build_cnf(n_frames: int, dim: int, sigma_min: float, base_scale: float, n_bl
     return FlowMatchingCNF(init=init, apply=apply, sample_base=sample_base,
                            get_x_t_and_conditional_u_t=partial(optimal_transport_conditional_vf, sigma_min=sigma_min),
                            log_prob_base=log_prob_base, sample_and_log_prob_base=sample_and_log_prob_base,
-                           cfg=cfg, device=dev, to_device=lambda params: device_params(params, cfg, dev))
+                           cfg=cfg, device=dev, to_device=to_device)
 
 
 def _param_count(cfg):
@@ -192,7 +203,7 @@ def sample_cnf(cnf: FlowMatchingCNF, params: Params, key, features=None, use_fix
                x0=None, solver: str = "dopri5", max_steps: int = 4096):
     """sample_and_log_prob.py:11-38: x0 ~ base, ODE 0 -> 1; returns x1 ([N*D] for one molecule, else [B, N*D])."""
     cfg = cnf.cfg
-    h = device_params(params, cfg, cnf.device)
+    h = cnf.to_device(params)
     if x0 is not None:
         x0 = torch.as_tensor(x0, device=cnf.device, dtype=torch.float32)
         squeeze = x0.dim() == 1
@@ -212,7 +223,7 @@ def get_log_prob(cnf: FlowMatchingCNF, params: Params, x, key, features=None, ap
 
     approx=False: exact trace of the full N*D Jacobian; approx=True: Hutchinson with eps ~ N(0, I) drawn once."""
     cfg = cnf.cfg
-    h = device_params(params, cfg, cnf.device)
+    h = cnf.to_device(params)
     x = torch.as_tensor(x, device=cnf.device, dtype=torch.float32)
     squeeze = x.dim() == 1
     x = x.reshape(-1, cfg.event_dim)
@@ -239,7 +250,7 @@ def sample_and_log_prob_cnf(cnf: FlowMatchingCNF, params: Params, key, features=
     As in the reference, the Hutchinson probe is the same standard-normal draw z that produced x0
     (sample_and_log_prob.py:130 vs :137)."""
     cfg = cnf.cfg
-    h = device_params(params, cfg, cnf.device)
+    h = cnf.to_device(params)
     if z is not None:
         z = torch.as_tensor(z, device=cnf.device, dtype=torch.float32)
         squeeze = z.dim() == 1

@@ -125,9 +125,14 @@ def init_params(cfg: CNFConfig, seed: int = 0) -> Dict[str, np.ndarray]:
     """flax-default-like initialisation (cnf.init, build_cnf.py:97): lecun-normal kernels, zero biases,
     variance_scaling(0.001, fan_avg, uniform) for the phi_x output layer (egnn.py:83-85), final_scaling 1.
     numpy PCG64 stands in for JAX threefry (not bit-compatible)."""
+    return init_from_spec(param_spec(cfg), seed)
+
+
+def init_from_spec(spec: List[Tuple[str, Tuple[int, ...]]], seed: int = 0) -> Dict[str, np.ndarray]:
+    """init_params over any (path, shape) tree (param_spec, or ref_param_spec for unequal widths)."""
     rng = np.random.Generator(np.random.PCG64(seed))
     p: Dict[str, np.ndarray] = {}
-    for path, shape in param_spec(cfg):
+    for path, shape in spec:
         parts = path.split("/")
         if parts[-1] == "bias":
             p[path] = np.zeros(shape, np.float32)
@@ -145,3 +150,118 @@ def init_params(cfg: CNFConfig, seed: int = 0) -> Dict[str, np.ndarray]:
                 z[bad] = rng.standard_normal(int(bad.sum()))
             p[path] = (z / np.sqrt(shape[0]) / 0.87962566103423978).astype(np.float32)
     return p
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# networks of any mlp_units / hidden width on the compiled kernel shapes (zero padding)
+# ---------------------------------------------------------------------------------------------------------------
+# (M, L, D) of the compiled kernels (ecnf_kernels.hpp ECNF_SHAPES / ECNF_SHAPES_WIDE_TAN)
+COMPILED_SHAPES = {(128, 3, 3), (128, 3, 2), (128, 2, 3), (128, 2, 2), (64, 2, 3), (64, 2, 2), (64, 3, 3), (64, 3, 2),
+                   (256, 4, 3), (256, 3, 3)}
+
+
+def ref_param_spec(n_features: int, hidden: int, time_embedding_dim: int, mlp_units, n_blocks: int
+                   ) -> List[Tuple[str, Tuple[int, ...]]]:
+    """The reference's parameter tree for ANY mlp_units (egnn.py:43-47: phi_e = MLP(mlp_units), phi_x_torso =
+    MLP(mlp_units) on m_ij of width mlp_units[-1], phi_h = MLP((*mlp_units, H)) on [m_i | h]; build_cnf.py:79,85)."""
+    H, T, K, U = hidden, time_embedding_dim, n_blocks, tuple(int(u) for u in mlp_units)
+    L = len(U)
+    shapes: Dict[Tuple[str, ...], Tuple[int, ...]] = {}
+
+    def dense(path, fan_in, fan_out):
+        shapes[path + ("bias",)] = (fan_out,)
+        shapes[path + ("kernel",)] = (fan_in, fan_out)
+
+    hu = U + (H,)
+    for k in range(K):
+        blk = ("EGNN_0", str(k))
+        dense(blk + ("Dense_0",), U[-1], 1)
+        dense(blk + ("Dense_1",), U[-1], 1)
+        for l in range(L):
+            dense(blk + ("phi_e", f"Dense_{l}"), 2 * H + 1 if l == 0 else U[l - 1], U[l])
+        for l in range(L + 1):
+            dense(blk + ("phi_h", f"Dense_{l}"), U[-1] + H if l == 0 else hu[l - 1], hu[l])
+        for l in range(L):
+            dense(blk + ("phi_x_torso", f"Dense_{l}"), U[-1] if l == 0 else U[l - 1], U[l])
+        dense(("EGNN_0", f"Dense_{k}"), H + T, H)
+    shapes[("EGNN_0", "final_scaling")] = ()
+    shapes[("Embed_0", "embedding")] = (n_features, H)
+    return [("/".join(p), shapes[p]) for p in sorted(shapes)]
+
+
+def kernel_config(n_nodes: int, dim: int, n_features: int, hidden: int, time_embedding_dim: int, mlp_units,
+                  n_blocks: int, base_scale: float = 1.0, sigma_min: float = 0.01) -> CNFConfig:
+    """The compiled kernel shape that runs a network of these widths: every MLP layer padded to the smallest compiled
+    width M >= max(mlp_units) for its depth and dim, the node features to a multiple of 32.  Zero-padded units are
+    inert: their pre-activations are exactly 0, SiLU(0) = 0, and every weight reading them is 0, so the padded network
+    computes the same function (the extra terms add exact zeros)."""
+    U = tuple(int(u) for u in mlp_units)
+    if not U or min(U) < 1:
+        raise ValueError("mlp_units must be a non-empty sequence of positive widths")
+    L = len(U)
+    fits = sorted(m for (m, l, d) in COMPILED_SHAPES if l == L and d == dim and m >= max(U))
+    if not fits:
+        raise ValueError(f"no compiled kernel for mlp_units={U} (depth {L}, width <= 256) at dim {dim}; compiled "
+                         f"(M, L, D): {sorted(COMPILED_SHAPES)}")
+    return CNFConfig(n_nodes=n_nodes, dim=dim, n_features=n_features, hidden=32 * ((int(hidden) + 31) // 32),
+                     time_embedding_dim=time_embedding_dim, mlp_width=fits[0], mlp_depth=L, n_blocks=n_blocks,
+                     base_scale=base_scale, sigma_min=sigma_min)
+
+
+def pad_params(params: Mapping, hidden: int, time_embedding_dim: int, mlp_units, kcfg: CNFConfig
+               ) -> Dict[str, np.ndarray]:
+    """Reference-shaped params (ref_param_spec) -> the zero-padded params of the kernel shape kcfg (kernel_config):
+    every [in, out] matrix is placed into the padded one by the row / column maps of its concatenated inputs
+    ([h_s | h_r | |r|^2] for phi_e.0, [m_i | h] for phi_h.0, [h | temb] for the node Dense)."""
+    flat = _flat_lookup(params)
+    H, T, U = int(hidden), int(time_embedding_dim), tuple(int(u) for u in mlp_units)
+    Hp, Mp, L = kcfg.hidden, kcfg.mlp_width, len(U)
+    hu, hup = U + (H,), (Mp,) * L + (Hp,)
+    spec = dict(ref_param_spec(kcfg.n_features, H, T, U, kcfg.n_blocks))
+    for path, shape in spec.items():
+        if path not in flat:
+            raise ValueError(f"missing parameter {path}")
+        if np.asarray(flat[path]).shape != shape:
+            raise ValueError(f"parameter {path} has shape {np.asarray(flat[path]).shape}, expected {shape}")
+    out: Dict[str, np.ndarray] = {}
+
+    def place(path, pshape, rows=None):
+        """rows: list of (src_lo, src_hi, dst_lo) row segments of a kernel (None: rows 0..n -> 0..n)."""
+        a = np.asarray(flat[path], np.float32)
+        z = np.zeros(pshape, np.float32)
+        if a.ndim == 1:
+            z[: a.shape[0]] = a
+        elif rows is None:
+            z[: a.shape[0], : a.shape[1]] = a
+        else:
+            for s0, s1, d0 in rows:
+                z[d0:d0 + s1 - s0, : a.shape[1]] = a[s0:s1]
+        out[path] = z
+
+    for k in range(kcfg.n_blocks):
+        b = f"EGNN_0/{k}"
+        for nm in ("Dense_0", "Dense_1"):
+            place(f"{b}/{nm}/kernel", (Mp, 1))
+            place(f"{b}/{nm}/bias", (1,))
+        for l in range(L):
+            if l == 0:
+                place(f"{b}/phi_e/Dense_0/kernel", (2 * Hp + 1, Mp), [(0, H, 0), (H, 2 * H, Hp), (2 * H, 2 * H + 1, 2 * Hp)])
+            else:
+                place(f"{b}/phi_e/Dense_{l}/kernel", (Mp, Mp))
+            place(f"{b}/phi_e/Dense_{l}/bias", (Mp,))
+            place(f"{b}/phi_x_torso/Dense_{l}/kernel", (Mp, Mp))
+            place(f"{b}/phi_x_torso/Dense_{l}/bias", (Mp,))
+        for l in range(L + 1):
+            if l == 0:
+                place(f"{b}/phi_h/Dense_0/kernel", (Mp + Hp, Mp), [(0, U[-1], 0), (U[-1], U[-1] + H, Mp)])
+            else:
+                place(f"{b}/phi_h/Dense_{l}/kernel", (Mp, hup[l]))
+            place(f"{b}/phi_h/Dense_{l}/bias", (hup[l],))
+        place(f"EGNN_0/Dense_{k}/kernel", (Hp + T, Hp), [(0, H, 0), (H, H + T, Hp)])
+        place(f"EGNN_0/Dense_{k}/bias", (Hp,))
+    out["EGNN_0/final_scaling"] = np.asarray(flat["EGNN_0/final_scaling"], np.float32).reshape(())
+    e = np.asarray(flat["Embed_0/embedding"], np.float32)
+    out["Embed_0/embedding"] = np.zeros((kcfg.n_features, Hp), np.float32)
+    out["Embed_0/embedding"][:, :H] = e
+    del hu
+    return out

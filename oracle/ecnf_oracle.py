@@ -75,10 +75,15 @@ class CNFConfig:
     sigma_min: float = 0.01
     normalization_constant: float = 1.0   # egnn.py:127
     variance_scaling_init: float = 0.001  # egnn.py:128
+    mlp_units: Optional[Tuple[int, ...]] = None   # unequal widths (egnn.py:43-47); None: (mlp_width,) * mlp_depth
 
     @property
     def n_edges(self) -> int:
         return self.n_nodes * (self.n_nodes - 1)
+
+    @property
+    def units(self) -> Tuple[int, ...]:
+        return tuple(self.mlp_units) if self.mlp_units else (self.mlp_width,) * self.mlp_depth
 
 
 # the configs of BASELINE.json, with shapes from examples/config/{dw4,lj13,aldp,qm9}.yaml
@@ -103,7 +108,9 @@ def param_spec(cfg: CNFConfig) -> List[Tuple[str, Tuple[int, ...]]]:
 
     Names follow flax auto-naming at ``build_cnf.py:79,85``, ``egnn.py:42-47,83,99,167-168,188``,
     ``mlp.py:13-16``."""
-    H, T, M, L, K = cfg.hidden, cfg.time_embedding_dim, cfg.mlp_width, cfg.mlp_depth, cfg.n_blocks
+    H, T, K = cfg.hidden, cfg.time_embedding_dim, cfg.n_blocks
+    U = cfg.units                           # mlp_units (egnn.py:43-47); m_ij has width U[-1]
+    L = len(U)
     tree: Dict[str, Tuple[int, ...]] = {}
 
     def dense(prefix, fan_in, fan_out):
@@ -112,14 +119,15 @@ def param_spec(cfg: CNFConfig) -> List[Tuple[str, Tuple[int, ...]]]:
 
     for k in range(K):
         blk = f"EGNN_0/{k}"
-        dense(f"{blk}/Dense_0", M, 1)       # phi_x output layer (egnn.py:83-85)
-        dense(f"{blk}/Dense_1", M, 1)       # gate (egnn.py:99)
+        dense(f"{blk}/Dense_0", U[-1], 1)   # phi_x output layer (egnn.py:83-85)
+        dense(f"{blk}/Dense_1", U[-1], 1)   # gate (egnn.py:99)
         for l in range(L):                  # phi_e (egnn.py:43)
-            dense(f"{blk}/phi_e/Dense_{l}", 2 * H + 1 if l == 0 else M, M)
+            dense(f"{blk}/phi_e/Dense_{l}", 2 * H + 1 if l == 0 else U[l - 1], U[l])
+        hu = U + (H,)
         for l in range(L + 1):              # phi_h = MLP((*mlp_units, H)) (egnn.py:46)
-            dense(f"{blk}/phi_h/Dense_{l}", M + H if l == 0 else M, H if l == L else M)
+            dense(f"{blk}/phi_h/Dense_{l}", U[-1] + H if l == 0 else hu[l - 1], hu[l])
         for l in range(L):                  # phi_x_torso (egnn.py:45)
-            dense(f"{blk}/phi_x_torso/Dense_{l}", M, M)
+            dense(f"{blk}/phi_x_torso/Dense_{l}", U[-1] if l == 0 else U[l - 1], U[l])
         dense(f"EGNN_0/Dense_{k}", H + T, H)  # per-block node Dense (egnn.py:167)
     tree["EGNN_0/final_scaling"] = ()
     tree["Embed_0/embedding"] = (cfg.n_features, H)
@@ -278,7 +286,7 @@ def _egcl(cfg, params, blk, vec, dvec, h, dh, dtype):
     if dh is not None:
         dedge_in = np.concatenate([dh[:, :, senders], dh[:, :, receivers], dlen2], axis=-1)
 
-    L = cfg.mlp_depth
+    L = len(cfg.units)
     m, dm = _mlp(edge_in, dedge_in, params, f"{blk}/phi_e", L, True, dtype)          # egnn.py:79
     px, dpx = _mlp(m, dm, params, f"{blk}/phi_x_torso", L, True, dtype)               # egnn.py:82
     px, dpx = _dense(px, dpx, params, f"{blk}/Dense_0", dtype)                         # egnn.py:83-85

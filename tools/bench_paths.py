@@ -3,8 +3,11 @@
 Each line: config, batch, solver, divergence, ms per launch (median of REPS HIP-event timings on the launch stream),
 molecules/s, mean NFE per molecule, and achieved algorithmic TFLOP/s counting (1 + tangents) x F per evaluation
 (F = bench.live_flops_per_eval; Hutchinson = 1 tangent, exact = N*D tangents).  Synthetic seeded inputs, flax-default
-random-init weights.  Usage: [ECNF_PATHS_ONLY=qm9,aldp] python tools/bench_paths.py [out.json]
+random-init weights.  Usage: python tools/bench_paths.py [--only qm9,aldp] [--div exact] [--case ID] [--reps R]
+[--out out.json]; ID is the case id printed in each line (e.g. lj13_b1024_euler_hutchinson_sample).  tools/
+profile_configs.sh runs single cases under rocprofv3 (kernel trace + counter passes) for profiles/.
 """
+import argparse
 import json
 import os
 import sys
@@ -38,6 +41,10 @@ CASES = [
 DIV = {"none": _lib.DIV_NONE, "hutchinson": _lib.DIV_HUTCHINSON, "exact": _lib.DIV_EXACT}
 
 
+def case_id(name, B, solver, step, div, direction):
+    return f"{name}_b{B}_{solver if step else 'pid'}_{div}_{direction}"
+
+
 def run_case(name, B, solver, step, div, direction):
     cfg = CONFIGS[name]
     h = EcnfHandle(cfg, init_params(cfg, 0), 0)
@@ -63,7 +70,7 @@ def run_case(name, B, solver, step, div, direction):
     nfe_mean = float(nfe.float().mean())
     tangents = {"none": 0, "hutchinson": 1, "exact": cfg.event_dim}[div]
     flop = B * nfe_mean * live_flops_per_eval(cfg) * (1 + tangents)
-    rec = {"config": name, "batch": B, "solver": solver, "step": step, "divergence": div, "direction": direction,
+    rec = {"case": case_id(name, B, solver, step, div, direction), "config": name, "batch": B, "solver": solver, "step": step, "divergence": div, "direction": direction,
            "ms": round(ms, 3), "molecules_per_s": round(B / ms * 1e3, 1), "nfe_mean": round(nfe_mean, 2),
            "tflops": round(flop / ms / 1e9, 2), "bad_status": int((st != 0).sum()),
            "finite": bool(torch.isfinite(y1).all()),
@@ -74,21 +81,30 @@ def run_case(name, B, solver, step, div, direction):
 
 
 def main():
+    global REPS
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="", help="comma-separated config names")
+    ap.add_argument("--div", default="", help="comma-separated divergence kinds")
+    ap.add_argument("--case", default="", help="one case id")
+    ap.add_argument("--reps", type=int, default=REPS)
+    ap.add_argument("--out", default="")
+    args = ap.parse_args()
+    REPS = args.reps
     out = []
-    only = os.environ.get("ECNF_PATHS_ONLY")   # comma-separated config names
-    divs = os.environ.get("ECNF_PATHS_DIV")    # comma-separated divergence kinds
     for case in CASES:
-        if only and case[0] not in only.split(","):
+        if args.only and case[0] not in args.only.split(","):
             continue
-        if divs and case[4] not in divs.split(","):
+        if args.div and case[4] not in args.div.split(","):
+            continue
+        if args.case and case_id(*case) != args.case:
             continue
         t = time.time()
         rec = run_case(*case)
         rec["wall_s"] = round(time.time() - t, 1)
         print(json.dumps(rec), flush=True)
         out.append(rec)
-    if len(sys.argv) > 1:
-        with open(sys.argv[1], "w") as f:
+    if args.out:
+        with open(args.out, "w") as f:
             json.dump(out, f, indent=1)
 
 
