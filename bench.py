@@ -407,27 +407,20 @@ def main():
         xb = h.base_sample(torch.randn((args.train_batch, cfg.event_dim), generator=gtr, device=dev))
         tt = torch.rand((args.train_batch,), generator=gtr, device=dev)
         ft = torch.zeros((args.train_batch, cfg.n_nodes), device=dev, dtype=torch.int32)
-        def run_steps(fn, n_steps):
-            torch.cuda.synchronize(dev)
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            for i in range(n_steps + 2):
-                if i == 2:
-                    e0.record(stream)
-                loss, grad = fn()
-                tr.adam_update(grad, p, mu, nu, None, lr=1e-4, count=i + 1)
-            e1.record(stream)
-            torch.cuda.synchronize(dev)
-            return e0.elapsed_time(e1) / n_steps, loss
-
-        ms_eager, loss = run_steps(lambda: tr.loss_and_grad(p, xd, xb, tt, ft), args.train_steps)
-        # the same step replayed from a captured HIP graph (one launch for the ~80 kernels of loss + gradient)
-        graphed = tr.graphed_loss_and_grad(p, args.train_batch)
-        ms, loss = run_steps(lambda: graphed(xd, xb, tt, ft), args.train_steps)
+        for i in range(args.train_steps + 2):
+            if i == 2:
+                torch.cuda.synchronize(dev)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+            loss, grad = tr.loss_and_grad(p, xd, xb, tt, ft)
+            tr.adam_update(grad, p, mu, nu, None, lr=1e-4, count=i + 1)
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        ms = e0.elapsed_time(e1) / args.train_steps
         train = {"workload": f"{args.config} flow-matching training step (loss + reverse-mode gradient + Adam), "
                              f"batch {args.train_batch}, strict-fp32 MFMA GEMMs",
-                 "ms_per_step": ms, "ms_per_step_eager_launches": ms_eager, "steps_per_s": 1e3 / ms,
-                 "molecules_per_s": args.train_batch * 1e3 / ms, "loss": float(loss),
-                 "launch": "loss + gradient replayed from a captured HIP graph, Adam launched eagerly"}
+                 "ms_per_step": ms, "steps_per_s": 1e3 / ms, "molecules_per_s": args.train_batch * 1e3 / ms,
+                 "loss": float(loss)}
 
     # HBM traffic, effective clock and MFMA occupancy of this workload's kernel, from counter passes run now
     pmc = None

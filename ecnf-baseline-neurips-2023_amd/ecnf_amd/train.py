@@ -97,46 +97,6 @@ class Trainer:
                                               _ptr(loss), _ptr(grad), self._stream()))
         return loss[0], grad
 
-    def graphed_loss_and_grad(self, params: torch.Tensor, batch: int, sigma_min: Optional[float] = None):
-        """The loss-and-gradient step of a fixed batch size captured once as a HIP graph (torch.cuda.CUDAGraph over
-        the library's stream-ordered launches: ~80 kernels per step for LJ13, replayed with one launch).  ``params``
-        must be the flat device blob the step will keep using (Adam updates it in place, so its address is stable).
-        Returns step(x1, x0, t, features) -> (loss, grad): the inputs are copied into the graph's static buffers;
-        loss / grad are the graph's output buffers, overwritten by the next replay."""
-        cfg = self.cfg
-        if not (torch.is_tensor(params) and params.is_cuda and params.numel() == self.n_params and
-                params.is_contiguous()):
-            raise ValueError("params must be the contiguous flat device blob of the training state")
-        B = int(batch)
-        if B < 1 or B > self.max_batch:
-            raise ValueError(f"batch must lie in [1, {self.max_batch}]")
-        sx1 = torch.zeros((B, cfg.event_dim), device=self.device)
-        sx0 = torch.zeros((B, cfg.event_dim), device=self.device)
-        st = torch.full((B,), 0.5, device=self.device)
-        sf = torch.zeros((B, cfg.n_nodes), device=self.device, dtype=torch.int32)
-        side = torch.cuda.Stream(self.device)
-        side.wait_stream(torch.cuda.current_stream(self.device))
-        with torch.cuda.stream(side):          # warm-up launch outside the capture (lazy library / kernel setup)
-            self.loss_and_grad(params, sx1, sx0, st, sf, sigma_min)
-        torch.cuda.current_stream(self.device).wait_stream(side)
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            loss, grad = self.loss_and_grad(params, sx1, sx0, st, sf, sigma_min)
-
-        def step(x1, x0, t, features):
-            sx1.copy_(torch.as_tensor(x1, device=self.device, dtype=torch.float32).reshape(B, cfg.event_dim))
-            sx0.copy_(torch.as_tensor(x0, device=self.device, dtype=torch.float32).reshape(B, cfg.event_dim))
-            st.copy_(torch.as_tensor(t, device=self.device, dtype=torch.float32).reshape(B))
-            f = torch.as_tensor(features)
-            if not f.is_cuda and f.numel() and (int(f.min()) < 0 or int(f.max()) >= cfg.n_features):
-                raise ValueError(f"feature ids must lie in [0, {cfg.n_features})")
-            sf.copy_(f.to(self.device, torch.int32).reshape(-1, cfg.n_nodes).expand(B, -1))
-            graph.replay()
-            return loss, grad
-
-        step.graph = graph
-        return step
-
     def adam_update(self, grad, params, mu, nu, ema, lr: float, count: int, b1: float = 0.9, b2: float = 0.999,
                     eps: float = 1e-8, eps_root: float = 0.0, ema_beta: float = 0.999):
         """In place: params, mu, nu (and ema when given).  Returns the device float[2] (|grad|, |update|)."""

@@ -169,19 +169,3 @@ def test_update_fn_trains_and_refreshes_the_sampler():
                        torch.from_numpy(feat[:4]).cuda()).cpu().numpy()
     ref = O.egnn_vector_field(trained, oc, data[:4], t, feat[:4], dtype=np.float64)
     assert np.abs(v - ref).max() <= 2e-5 * max(1.0, np.abs(ref).max())
-
-
-def test_graphed_step_matches_eager():
-    """The HIP-graph replay of the loss-and-gradient step (Trainer.graphed_loss_and_grad) gives bitwise the eager
-    step's loss and gradient, for new inputs on every replay (the kernels are deterministic)."""
-    cfg = CONFIGS["lj13"]
-    oc, p, x1, x0, t, feat = _case(cfg, 8)
-    tr = TR.Trainer(cfg, max_batch=8, device=0)
-    pd = tr.device_params(p)
-    step = tr.graphed_loss_and_grad(pd, 8)
-    for seed in (0, 1):
-        _, _, a1, a0, at, af = _case(cfg, 8, seed=seed + 10)
-        le, ge = tr.loss_and_grad(pd, a1, a0, at, af)
-        lg, gg = step(a1, a0, at, af)
-        torch.cuda.synchronize()
-        assert torch.equal(le, lg) and torch.equal(ge, gg)
