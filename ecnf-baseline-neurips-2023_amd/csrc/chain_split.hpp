@@ -210,6 +210,12 @@ struct ChainInv {
 #ifndef ECNF_SPLIT_PF
 #define ECNF_SPLIT_PF 3
 #endif
+#ifndef ECNF_SPLIT_PF3   // weight groups in flight for the 3-piece (exact-weight) chains
+#define ECNF_SPLIT_PF3 3
+#endif
+#ifndef ECNF_SPLIT_PF3_NARROW   // ... at M = 64, where the kernel runs 2 waves per SIMD (ALDP A/B: 50.5 -> 50.2 ms)
+#define ECNF_SPLIT_PF3_NARROW 2
+#endif
 // the activation's stage-B add and stage-C multiply as packed fp32 (v_pk_add_f32 / v_pk_mul_f32) where the compiler
 // keeps the pair in an aligned register pair (bit-identical; LJ13 27.14 -> 27.02 ms A/B, profiles/round2/e3);
 // -DECNF_SPLIT_NO_PK: scalar
@@ -274,7 +280,8 @@ __device__ __forceinline__ void chain_split(SplitX<NF>& XA, SplitX<NF>& XB, f32x
 #endif
   // the chain wave issues first on its SIMD while its partner wave is in VALU / LDS work (A/B: 26.14 -> 25.99 ms)
   __builtin_amdgcn_s_setprio(ECNF_CHAIN_PRIO);
-  constexpr int GB = Plan::GB, GL = Plan::GL, G = Plan::G, NI = Plan::NI, PF = ECNF_SPLIT_PF;
+  constexpr int GB = Plan::GB, GL = Plan::GL, G = Plan::G, NI = Plan::NI,
+                PF = WP == 3 ? (NF <= 2 ? ECNF_SPLIT_PF3_NARROW : ECNF_SPLIT_PF3) : ECNF_SPLIT_PF;
   constexpr int GE = Plan::last_group() + 1;   // groups including the VALU-only tail
   const int kk = lane >> 5;
   const float* lbias = bias + 4 * kk;
@@ -688,7 +695,7 @@ __device__ __forceinline__ void dual_pass(const SplitX<NF>& X, f32x16 (&acc)[NF]
 template <int NF, int NL>
 __device__ __forceinline__ void chain_dual_seq(f32x16 (&X)[NF], f32x16 (&XT)[NF], const unsigned* __restrict__ Wpk,
                                                const float* __restrict__ bias, const float* cinv, int lane,
-                                               bool in_log2) {
+                                               bool in_log2, bool out_log2 = false) {
   constexpr float kNegLog2e = -1.4426950408889634f, kNegLn2 = -0.69314718055994531f;
   constexpr int WP = 3;   // exact 3-piece weights (chain_split WP = 3)
   const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned*>(Wpk), (short)0,
@@ -741,6 +748,7 @@ __device__ __forceinline__ void chain_dual_seq(f32x16 (&X)[NF], f32x16 (&XT)[NF]
       }
     __builtin_amdgcn_sched_barrier(0);
   }
+  if (out_log2) return;   // the split tangent kernels' log2-domain tail (w_g', w_x' carry the -ln 2)
 #pragma unroll
   for (int fb = 0; fb < NF; ++fb)
 #pragma unroll

@@ -81,12 +81,22 @@ struct Geo {
 #ifndef ECNF_SPLIT_NW
 #define ECNF_SPLIT_NW 8
 #endif
-  static constexpr int NW = (NT == 0 && NF <= 4) ? (kSplit ? ECNF_SPLIT_NW : 8) : 4;
+#ifndef ECNF_TAN_NW_NF2
+#define ECNF_TAN_NW_NF2 8
+#endif
+  // M = 64 tangent kernels (ALDP): 8 waves, 2 per SIMD at <= 256 registers, so one wave's VALU phases (layer-1
+  // assembly, gate / aggregation scans, shifts: twice the VALU per MFMA of M = 128) overlap the other's chain
+  // (ALDP B = 512 PID Hutchinson log_prob 61.8 -> 50.2 ms, outputs bitwise equal; 72 B/lane of spills outside the
+  // chain)
+  // (M = 128 at 8 waves: even with sequential primal / tangent chain passes, chain_dual_seq, the kernel spilled
+  // 1.2 KB per lane at 256 registers; it stays at 4 waves)
+  static constexpr int NW = (NT == 0 && NF <= 4) ? (kSplit ? ECNF_SPLIT_NW : 8)
+                            : (NT == 1 && P == 0 && NF <= 2 ? ECNF_TAN_NW_NF2 : 4);
   static constexpr int NTHR = 64 * NW;
   // minimum waves per SIMD the register allocation must allow: 2 only for 2 x 4-wave workgroups per CU of the M <= 128
   // split primal kernels at -DECNF_SPLIT_NW=4.  (The M = 256 split primal kernels also run 4 waves, but need their
   // 512 registers: at 2 waves per SIMD they spilled 968 B per lane and QM9 B = 2048 Euler-100 ran 2162 -> 3423 ms.)
-  static constexpr int WPE = (kSplit && NF <= 4 && NW == 4) ? 2 : 1;
+  static constexpr int WPE = ((kSplit && NF <= 4 && NW == 4) || (NT == 1 && NW == 8)) ? 2 : 1;
 };
 constexpr int kMaxBlocks = 10;
 constexpr int kMaxPhiH = 5;     // L + 1 <= 5
