@@ -22,6 +22,7 @@
 //   z_h / a_h [L+1][BN][M|H] (phi_h)
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <string>
@@ -48,7 +49,14 @@ __device__ __forceinline__ float dsilu(float z) {
 // GEMM: C[M][N] = alpha op(A)[M][K] op(B)[K][N] (+ bias[N]) (+ R) (+ C if accumulate), then optionally
 // z *= silu'(Zs) (the backward of a SiLU layer) and Aout = silu(z) (the forward one, C keeps the pre-activation).
 // TA: A stored [K][M] (lda over m); TB: B stored [N][K].  ksplit > 1: block z sums its k-range into the partial
-// C + z * split_stride (no epilogue), combined by reduce_splits in split order.
+// C + z * split_stride (no epilogue), combined by reduce_splits in split order.  colsum (weight gradients, TA && !TB):
+// the column sums of B over the block's k-range (the bias gradient sum_k dZ[k][n]), written by the first m-tile's
+// wave 0 into colsum[n] (ksplit == 1) or colsum_part[z][n].
+//
+// 64x64 tile per 256-thread workgroup (4 waves of 32x32 on v_mfma_f32_32x32x2_f32), 32-deep k tiles double-buffered
+// in LDS with the next tile's global loads in flight (registers) while the current one is multiplied.  Both operands
+// are staged k-contiguous ([m][k], [n][k], row stride 33): the MFMA operand reads (32 rows x 2 k per wave) and the
+// stores of either source layout touch distinct banks.
 // ---------------------------------------------------------------------------------------------------------------
 struct GemmArgs {
   int M, N, K;
@@ -62,14 +70,15 @@ struct GemmArgs {
   float* Aout; long ldo;
   int accumulate;
   int ksplit; long split_stride;
+  float* colsum; float* colsum_part;
 };
 
-constexpr int GT = 64, GK = 16;
+constexpr int GT = 64, GK = 32, GS = GK + 1, GE = GT * GK / 256;   // GE: elements per thread per operand tile
 
 template <bool TA, bool TB>
 __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
-  __shared__ float As[GK][GT + 1];
-  __shared__ float Bs[GK][GT + 1];
+  __shared__ float As[2][GT * GS];
+  __shared__ float Bs[2][GT * GS];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int m0 = blockIdx.y * GT, n0 = blockIdx.x * GT;
   const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
@@ -79,32 +88,67 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
     kb = blockIdx.z * kc;
     ke = min(g.K, kb + kc);
   }
-  f32x16 acc = {};
-  for (int k0 = kb; k0 < ke; k0 += GK) {
-    for (int i = tid; i < GT * GK; i += 256) {
-      int mm, kk;
-      if (TA) { mm = i % GT; kk = i / GT; } else { kk = i % GK; mm = i / GK; }
-      const int gm = m0 + mm, gk = k0 + kk;
-      float v = 0.f;
-      if (gm < g.M && gk < ke) v = TA ? g.A[(long)gk * g.lda + gm] : g.A[(long)gm * g.lda + gk];
-      As[kk][mm] = v;
-    }
-    for (int i = tid; i < GT * GK; i += 256) {
-      int nn, kk;
-      if (TB) { kk = i % GK; nn = i / GK; } else { nn = i % GT; kk = i / GT; }
-      const int gn = n0 + nn, gk = k0 + kk;
-      float v = 0.f;
-      if (gn < g.N && gk < ke) v = TB ? g.B[(long)gn * g.ldb + gk] : g.B[(long)gk * g.ldb + gn];
-      Bs[kk][nn] = v;
-    }
-    __syncthreads();
+  // element e of this thread's share: (row within the tile, k within the tile), source-coalesced
+  auto a_idx = [&](int e, int& mm, int& kk) {
+    const int i = tid + 256 * e;
+    if (TA) { mm = i % GT; kk = i / GT; } else { kk = i % GK; mm = i / GK; }
+  };
+  auto b_idx = [&](int e, int& nn, int& kk) {
+    const int i = tid + 256 * e;
+    if (TB) { kk = i % GK; nn = i / GK; } else { nn = i % GT; kk = i / GT; }
+  };
+  float ra[GE], rb[GE];
+  auto load = [&](int k0) {
 #pragma unroll
-    for (int kk = 0; kk < GK; kk += 2) {
-      const float a = As[kk + (lane >> 5)][wm + (lane & 31)];
-      const float b = Bs[kk + (lane >> 5)][wn + (lane & 31)];
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
+    for (int e = 0; e < GE; ++e) {
+      int mm, kk;
+      a_idx(e, mm, kk);
+      const int gm = m0 + mm, gk = k0 + kk;
+      ra[e] = (gm < g.M && gk < ke) ? (TA ? g.A[(long)gk * g.lda + gm] : g.A[(long)gm * g.lda + gk]) : 0.f;
+      int nn;
+      b_idx(e, nn, kk);
+      const int gn = n0 + nn, gk2 = k0 + kk;
+      rb[e] = (gn < g.N && gk2 < ke) ? (TB ? g.B[(long)gn * g.ldb + gk2] : g.B[(long)gk2 * g.ldb + gn]) : 0.f;
     }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int e = 0; e < GE; ++e) {
+      int mm, kk;
+      a_idx(e, mm, kk);
+      As[buf][mm * GS + kk] = ra[e];
+      int nn;
+      b_idx(e, nn, kk);
+      Bs[buf][nn * GS + kk] = rb[e];
+    }
+  };
+  const bool do_colsum = g.colsum && blockIdx.y == 0 && tid < GT;
+  float csum = 0.f;
+  f32x16 acc = {};
+  if (kb < ke) {
+    load(kb);
+    store(0);
+  }
+  __syncthreads();
+  int buf = 0;
+  for (int k0 = kb; k0 < ke; k0 += GK) {
+    const bool more = k0 + GK < ke;
+    if (more) load(k0 + GK);
+    const float* Ab = &As[buf][(wm + (lane & 31)) * GS + (lane >> 5)];
+    const float* Bb = &Bs[buf][(wn + (lane & 31)) * GS + (lane >> 5)];
+#pragma unroll
+    for (int kk = 0; kk < GK; kk += 2) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(Ab[kk], Bb[kk], acc, 0, 0, 0);
+    if (do_colsum) {
+#pragma unroll 8
+      for (int kk = 0; kk < GK; ++kk) csum += Bs[buf][tid * GS + kk];
+    }
+    if (more) store(buf ^ 1);
     __syncthreads();
+    buf ^= 1;
+  }
+  if (do_colsum && n0 + tid < g.N) {
+    if (g.ksplit > 1) g.colsum_part[(long)blockIdx.z * g.N + n0 + tid] = csum;
+    else g.colsum[n0 + tid] = csum;
   }
   const int col = n0 + wn + (lane & 31);
   if (col >= g.N) return;
@@ -126,23 +170,25 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
   }
 }
 
-// dst[i] (+)= sum_s P[s][i], s in order
-__global__ void reduce_splits(const float* __restrict__ P, int S, long n, float* dst, int accumulate) {
-  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+// dst[i] (+)= sum_s P[s][i], s in order; the n2 entries after the first n come from P2 [S][n2] into dst2 (the
+// column-sum partials of a weight-gradient GEMM reduced in the same launch)
+__global__ void reduce_splits(const float* __restrict__ P, int S, long n, float* dst, int accumulate,
+                              const float* __restrict__ P2, long n2, float* dst2) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n + n2) return;
+  const float* src = P;
+  float* out = dst;
+  long stride = n;
+  if (i >= n) {
+    i -= n;
+    src = P2;
+    out = dst2;
+    stride = n2;
+  }
   float acc = 0.f;
-  for (int s = 0; s < S; ++s) acc += P[(long)s * n + i];
-  dst[i] = accumulate ? dst[i] + acc : acc;
-}
-
-// column sums of X[rows][cols] (ld) in row chunks of 256: part[chunk][c]
-__global__ void colsum_kernel(const float* __restrict__ X, int rows, int cols, long ld, float* part) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= cols) return;
-  const int r0 = blockIdx.y * 256, r1 = min(rows, r0 + 256);
-  float acc = 0.f;
-  for (int r = r0; r < r1; ++r) acc += X[(long)r * ld + c];
-  part[(long)blockIdx.y * cols + c] = acc;
+#pragma unroll 4
+  for (int s = 0; s < S; ++s) acc += src[(long)s * stride + i];
+  out[i] = (accumulate && out == dst) ? out[i] + acc : acc;
 }
 
 // ---------------------------------------------------------------------------------------------------------------
@@ -168,32 +214,36 @@ struct Freqs {
   float f[8];   // exp(-k ln(1e4) / (T/2 - 1)) in fp32 (build_cnf.py:23-27)
 };
 
-// x_t, u_t (core.py:35-39), input mean, centred positions (egnn.py:160), time embedding (build_cnf.py:18-32)
+// x_t, u_t (core.py:35-39), input mean, centred positions (egnn.py:160), time embedding (build_cnf.py:18-32).  One
+// 64-thread block per molecule: coordinates one per thread, the per-dimension means summed over the nodes in order
+// (N * D <= kMaxND)
+constexpr int kMaxND = 256;
 __global__ void k_prologue(Geom G, const float* __restrict__ x1, const float* __restrict__ x0,
                            const float* __restrict__ t, Freqs freqs, float* ut, float* mean, float* xc0,
                            float* temb) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= G.B) return;
-  const int ND = G.N * G.D;
+  __shared__ float xs[kMaxND];
+  __shared__ float mu[3];
+  const int b = blockIdx.x, ND = G.N * G.D;
   const float tb = t[b];
-  float mu[3] = {0.f, 0.f, 0.f};
-  for (int i = 0; i < G.N; ++i)
-    for (int d = 0; d < G.D; ++d) {
-      const long o = (long)b * ND + i * G.D + d;
-      const float xt = (1.0f - (1.0f - G.sigma) * tb) * x0[o] + tb * x1[o];
-      ut[o] = x1[o] - (1.0f - G.sigma) * x0[o];
-      xc0[o] = xt;
-      mu[d] += xt;
-    }
-  for (int d = 0; d < G.D; ++d) {
-    mu[d] /= (float)G.N;
-    mean[b * G.D + d] = mu[d];
+  for (int k = threadIdx.x; k < ND; k += blockDim.x) {
+    const long o = (long)b * ND + k;
+    xs[k] = (1.0f - (1.0f - G.sigma) * tb) * x0[o] + tb * x1[o];
+    ut[o] = x1[o] - (1.0f - G.sigma) * x0[o];
   }
-  for (int i = 0; i < G.N; ++i)
-    for (int d = 0; d < G.D; ++d) xc0[(long)b * ND + i * G.D + d] -= mu[d];
+  __syncthreads();
+  if ((int)threadIdx.x < G.D) {
+    const int d = threadIdx.x;
+    float a = 0.f;
+    for (int i = 0; i < G.N; ++i) a += xs[i * G.D + d];
+    a /= (float)G.N;
+    mu[d] = a;
+    mean[b * G.D + d] = a;
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < ND; k += blockDim.x) xc0[(long)b * ND + k] = xs[k] - mu[k % G.D];
   const int half = G.T / 2;
   const float ts = tb * 1000.0f;
-  for (int k = 0; k < G.T; ++k) {
+  for (int k = threadIdx.x; k < G.T; k += blockDim.x) {
     const float arg = ts * freqs.f[k < half ? k : k - half];
     temb[b * G.T + k] = k < half ? sinf(arg) : cosf(arg);
   }
@@ -313,26 +363,32 @@ __global__ void k_node_agg(Geom G, const float* __restrict__ m, const float* __r
 }
 
 // v = ((x_K - x_c0) - mean) fs (egnn.py:183-188), per-molecule partial loss sum((v - u)^2) and d fs, and
-// d loss / d x_K = 2 (v - u) fs / (B N D)
+// d loss / d x_K = 2 (v - u) fs / (B N D).  One 64-thread block per molecule; the two sums in coordinate order
 __global__ void k_output(Geom G, const float* __restrict__ xK, const float* __restrict__ xc0,
                          const float* __restrict__ mean, const float* __restrict__ ut, const float* __restrict__ fs_p,
                          float* dxK, float* part_loss, float* part_dfs) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= G.B) return;
+  __shared__ float sq[kMaxND], sf[kMaxND];
+  const int b = blockIdx.x, ND = G.N * G.D;
   const float fs = fs_p[0];
-  const int ND = G.N * G.D;
   const float sc = 2.0f / ((float)G.B * (float)ND);
-  float sl = 0.f, sf = 0.f;
-  for (int k = 0; k < ND; ++k) {
+  for (int k = threadIdx.x; k < ND; k += blockDim.x) {
     const long o = (long)b * ND + k;
     const float pre = (xK[o] - xc0[o]) - mean[b * G.D + (k % G.D)];
     const float diff = pre * fs - ut[o];
-    sl += diff * diff;
-    sf += sc * diff * pre;
+    sq[k] = diff * diff;
+    sf[k] = sc * diff * pre;
     dxK[o] = sc * diff * fs;
   }
-  part_loss[b] = sl;
-  part_dfs[b] = sf;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float a = 0.f, c = 0.f;
+    for (int k = 0; k < ND; ++k) {
+      a += sq[k];
+      c += sf[k];
+    }
+    part_loss[b] = a;
+    part_dfs[b] = c;
+  }
 }
 
 __global__ void k_finish_loss(int B, float inv_count, const float* __restrict__ part_loss,
@@ -466,17 +522,27 @@ __global__ void k_dx_bwd(Geom G, const float* __restrict__ dxout, const float* _
   dxin[idx] = dxout[idx] + a - s;
 }
 
-// embedding gradient: dEmb[f][c] = sum over node rows with feature f of dhin[row][c] (rows in order)
+// embedding gradient: dEmb[f][c] = sum over node rows with feature f of dhin[row][c].  Partial sums over chunks of
+// 64 rows (256 threads = 4 row lanes x 64 columns; grid.x = n_features x column blocks, grid.y = row chunks), each
+// chunk's 4 lanes combined in order; the chunks are summed in order by reduce_splits: part[chunk][f H + c]
 __global__ void k_embed_bwd(Geom G, const float* __restrict__ dhin, long ld, const int32_t* __restrict__ feat,
-                            float* demb) {
-  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (long)G.nfeat * G.H) return;
-  const int f = (int)(idx / G.H), c = (int)(idx - (long)f * G.H);
+                            float* part) {
+  __shared__ float red[4][64];
+  const int hc = (G.H + 63) / 64;
+  const int f = blockIdx.x / hc, c = (blockIdx.x % hc) * 64 + (threadIdx.x & 63), rl = threadIdx.x >> 6;
+  const long BN = (long)G.B * G.N, r0 = (long)blockIdx.y * 64;
   float a = 0.f;
-  const long BN = (long)G.B * G.N;
-  for (long row = 0; row < BN; ++row)
-    if (feat[row] == f) a += dhin[row * ld + c];
-  demb[idx] = a;
+  if (c < G.H)
+    for (int j = 0; j < 16; ++j) {
+      const long row = r0 + rl + 4 * j;
+      if (row < BN && feat[row] == f) a += dhin[row * ld + c];
+    }
+  red[rl][threadIdx.x & 63] = a;
+  __syncthreads();
+  if (rl == 0 && c < G.H) {
+    const int q = threadIdx.x;
+    part[(long)blockIdx.y * G.nfeat * G.H + (long)f * G.H + c] = ((red[0][q] + red[1][q]) + red[2][q]) + red[3][q];
+  }
 }
 
 // ---- Adam (optax.scale_by_adam + scale(-lr)) and EMA, with the global norms of the gradient and the update ----
@@ -516,15 +582,28 @@ __global__ void k_adam(long n, const float* __restrict__ grad, float* params, fl
   }
 }
 
+// global norms from the Adam blocks' partials: one 256-thread block, strided partial sums then a fixed-order tree
 __global__ void k_norms(int nb, const float* __restrict__ part, float* norms) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  __shared__ float red[2][256];
   float a = 0.f, b = 0.f;
-  for (int i = 0; i < nb; ++i) {
+  for (int i = threadIdx.x; i < nb; i += 256) {
     a += part[2 * i];
     b += part[2 * i + 1];
   }
-  norms[0] = sqrtf(a);
-  norms[1] = sqrtf(b);
+  red[0][threadIdx.x] = a;
+  red[1][threadIdx.x] = b;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) {
+      red[0][threadIdx.x] += red[0][threadIdx.x + w];
+      red[1][threadIdx.x] += red[1][threadIdx.x + w];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    norms[0] = sqrtf(red[0][0]);
+    norms[1] = sqrtf(red[1][0]);
+  }
 }
 
 }  // namespace ecnf_train
@@ -597,8 +676,8 @@ struct ecnf_trainer {
   float *ut, *mean, *temb, *part_loss, *part_dfs, *dxa, *dxb, *norm_part;
   std::vector<float*> xc, hin, h1, Ps, Pr, r, len, px, gate, hcat;   // [K] (xc: [K + 1])
   std::vector<float*> ze, ae, zx, ax, zh, ah;                        // [K * L], [K * (L + 1)]
-  float *dA, *dB, *dm_gate, *de, *dpx, *dr, *dPs, *dPr, *dhcat, *dh1, *dhin, *dhA, *dhB, *dhn, *split;
-  size_t split_floats;
+  float *dA, *dB, *dm_gate, *de, *dpx, *dr, *dPs, *dPr, *dhcat, *dh1, *dhin, *dhA, *dhB, *dhn, *split, *csplit;
+  size_t split_floats, csplit_floats;
 };
 
 namespace {
@@ -617,32 +696,32 @@ struct Launcher {
   void gemm(bool ta, bool tb, int M, int N, int K, const float* A, long lda, const float* B, long ldb, float* C,
             long ldc, const float* bias = nullptr, const float* R = nullptr, long ldr = 0, const float* Zs = nullptr,
             long ldz = 0, float* Aout = nullptr, long ldo = 0, int accumulate = 0) {
-    GemmArgs g{M, N, K, A, lda, B, ldb, C, ldc, 1.0f, bias, R, ldr, Zs, ldz, Aout, ldo, accumulate, 1, 0};
+    GemmArgs g{M, N, K, A, lda, B, ldb, C, ldc, 1.0f, bias, R, ldr, Zs, ldz, Aout, ldo, accumulate, 1, 0,
+               nullptr, nullptr};
     dim3 grid(nblk(N, GT), nblk(M, GT), 1);
     launch(ta, tb, g, grid);
   }
-  // weight gradient dW[M][N] (= or +=) A^T dZ over K rows, split over the K dimension, reduced in order
+  // weight gradient dW[M][N] = A^T dZ over K rows and the bias gradient db[N] = sum_k dZ[k] (db may be NULL),
+  // split over the K dimension into >= ~384 workgroups of >= 128 rows, reduced in split order in one launch
   void gemm_wgrad(int M, int N, int K, const float* A, long lda, const float* dZ, long ldz, float* dW, long ldw,
-                  int accumulate = 0) {
+                  float* db = nullptr) {
     const long n = (long)M * N;
-    int S = (int)std::min<long>(64, std::max<long>(1, K / 256));
-    while (S > 1 && (long)S * n > (long)tr->split_floats) --S;
+    const long tiles = (long)nblk(M, GT) * nblk(N, GT);
+    int S = (int)std::min<long>({128, std::max<long>(1, (384 + tiles - 1) / tiles), std::max<long>(1, K / 128)});
+    while (S > 1 && ((long)S * n > (long)tr->split_floats || (long)S * N > (long)tr->csplit_floats)) --S;
     if (S == 1) {
-      GemmArgs g{M, N, K, A, lda, dZ, ldz, dW, ldw, 1.0f, nullptr, nullptr, 0, nullptr, 0, nullptr, 0, accumulate, 1, 0};
+      GemmArgs g{M, N, K, A, lda, dZ, ldz, dW, ldw, 1.0f, nullptr, nullptr, 0, nullptr, 0, nullptr, 0, 0, 1, 0,
+                 db, nullptr};
       launch(true, false, g, dim3(nblk(N, GT), nblk(M, GT), 1));
       return;
     }
-    GemmArgs g{M, N, K, A, lda, dZ, ldz, tr->split, N, 1.0f, nullptr, nullptr, 0, nullptr, 0, nullptr, 0, 0, S, n};
+    GemmArgs g{M, N, K, A, lda, dZ, ldz, tr->split, N, 1.0f, nullptr, nullptr, 0, nullptr, 0, nullptr, 0, 0, S, n,
+               db, tr->csplit};
     launch(true, false, g, dim3(nblk(N, GT), nblk(M, GT), S));
     // ldw == N for every weight block of the flat blob (row-major [in][out])
-    hipLaunchKernelGGL(reduce_splits, dim3(nblk(n)), dim3(256), 0, s, tr->split, S, n, dW, accumulate);
-    check();
-  }
-  void colsum(const float* X, int rows, int cols, long ld, float* out) {
-    const int chunks = (rows + 255) / 256;
-    hipLaunchKernelGGL(colsum_kernel, dim3(nblk(cols), chunks), dim3(256), 0, s, X, rows, cols, ld, tr->split);
-    check();
-    hipLaunchKernelGGL(reduce_splits, dim3(nblk(cols)), dim3(256), 0, s, tr->split, chunks, (long)cols, out, 0);
+    const long n2 = db ? N : 0;
+    hipLaunchKernelGGL(reduce_splits, dim3(nblk(n + n2)), dim3(256), 0, s, tr->split, S, n, dW, 0,
+                       (const float*)tr->csplit, n2, db);
     check();
   }
   void launch(bool ta, bool tb, const GemmArgs& g, dim3 grid) {
@@ -665,6 +744,7 @@ int ecnf_trainer_create(const ecnf_cfg* cfg, int32_t max_batch, int device, ecnf
   if (rc) return rc;
   if (!out) return fail(ECNF_E_INVALID, "out is NULL");
   if (max_batch < 1) return fail(ECNF_E_INVALID, "max_batch must be >= 1");
+  if (cfg->n_nodes * cfg->dim > kMaxND) return fail(ECNF_E_UNSUPPORTED, "training needs n_nodes * dim <= 256");
   const ecnf_cfg c = *cfg;
   const long B = max_batch, N = c.n_nodes, D = c.dim, H = c.hidden, T = c.time_embedding_dim, M = c.mlp_width,
              L = c.mlp_depth, K = c.n_blocks;
@@ -704,10 +784,13 @@ int ecnf_trainer_create(const ecnf_cfg* cfg, int32_t max_batch, int device, ecnf
   add(&tr->dr, BE * D); add(&tr->dPs, BN * M); add(&tr->dPr, BN * M); add(&tr->dhcat, BN * (M + H));
   add(&tr->dh1, BN * H); add(&tr->dhin, BN * (H + T)); add(&tr->dhA, BN * M); add(&tr->dhB, BN * M);
   add(&tr->dhn, BN * H);
-  // split-K / column-sum partials: up to 64 splits of the largest weight block ((M + H) x M or (2H + 1) x M) and
-  // the column-sum chunks of BE rows
-  tr->split_floats = (size_t)std::max<long>(64 * std::max((M + H) * M, (2 * H + 1) * M), ((BE + 255) / 256) * M + M);
+  // split-K partials: up to 128 splits of the largest weight block ((M + H) x M, (H + T) x H or 2H x M), their
+  // column sums (bias gradients), and the embedding gradient's row-chunk partials
+  tr->split_floats = (size_t)std::max<long>(128 * std::max({(M + H) * M, (H + T) * H, 2 * H * M}),
+                                            ((BN + 63) / 64) * (long)c.n_features * H);
   add(&tr->split, (long)tr->split_floats);
+  tr->csplit_floats = (size_t)(128 * std::max({M + H, H + T, M}));
+  add(&tr->csplit, (long)tr->csplit_floats);
   size_t total = 0;
   for (auto& q : plan) total += (size_t)q.second;
   tr->arena_floats = total;
@@ -762,7 +845,7 @@ int ecnf_fm_loss_grad(ecnf_trainer* tr, const float* params, const float* x1, co
   std::memcpy(fq.f, tr->freqs, sizeof(fq.f));
 
   // ------------------------------------------------------------------ forward
-  hipLaunchKernelGGL(k_prologue, dim3(nb(B)), dim3(256), 0, s, G, x1, x0, t, fq, tr->ut, tr->mean, tr->xc[0],
+  hipLaunchKernelGGL(k_prologue, dim3((unsigned)B), dim3(64), 0, s, G, x1, x0, t, fq, tr->ut, tr->mean, tr->xc[0],
                      tr->temb);
   Lc.check();
   for (long k = 0; k < K; ++k) {
@@ -815,7 +898,7 @@ int ecnf_fm_loss_grad(ecnf_trainer* tr, const float* params, const float* x1, co
       }
     }
   }
-  hipLaunchKernelGGL(k_output, dim3(nb(B)), dim3(256), 0, s, G, (const float*)tr->xc[K], (const float*)tr->xc[0],
+  hipLaunchKernelGGL(k_output, dim3((unsigned)B), dim3(64), 0, s, G, (const float*)tr->xc[K], (const float*)tr->xc[0],
                      (const float*)tr->mean, (const float*)tr->ut, P + o.fs, tr->dxa, tr->part_loss, tr->part_dfs);
   Lc.check();
   hipLaunchKernelGGL(k_finish_loss, dim3(1), dim3(64), 0, s, (int)B, 1.0f / (float)(B * ND),
@@ -838,8 +921,7 @@ int ecnf_fm_loss_grad(ecnf_trainer* tr, const float* params, const float* x1, co
       for (long l = L; l >= 0; --l) {
         const int in_f = (int)(l == 0 ? M + H : M), out_f = (int)(l == L ? H : M);
         const float* X = l == 0 ? tr->hcat[k] : tr->ah[k * (L + 1) + l - 1];
-        Lc.gemm_wgrad(in_f, out_f, (int)BN, X, in_f, dZ, out_f, dP + bo.hk[l], out_f);
-        Lc.colsum(dZ, (int)BN, out_f, out_f, dP + bo.hb[l]);
+        Lc.gemm_wgrad(in_f, out_f, (int)BN, X, in_f, dZ, out_f, dP + bo.hk[l], out_f, dP + bo.hb[l]);
         if (l > 0) {
           float* dZp = bufs[l & 1];
           Lc.gemm(false, true, (int)BN, (int)M, out_f, dZ, out_f, P + bo.hk[l], out_f, dZp, M, nullptr, nullptr, 0,
@@ -859,8 +941,7 @@ int ecnf_fm_loss_grad(ecnf_trainer* tr, const float* params, const float* x1, co
                        (const float*)tr->r[k], (const float*)tr->len[k], tr->dpx, tr->dr);
     Lc.check();
     // phi_x output Dense(1): dw_x = a_x[L-1]^T dpx, db_x = sum dpx; dZ_x[L-1] = dpx w_x silu'(z)
-    Lc.gemm_wgrad((int)M, 1, (int)BE, tr->ax[k * L + L - 1], M, tr->dpx, 1, dP + bo.xk, 1);
-    Lc.colsum(tr->dpx, (int)BE, 1, 1, dP + bo.xb);
+    Lc.gemm_wgrad((int)M, 1, (int)BE, tr->ax[k * L + L - 1], M, tr->dpx, 1, dP + bo.xk, 1, dP + bo.xb);
     hipLaunchKernelGGL(k_outer_dsilu, dim3(nb(BE * M)), dim3(256), 0, s, BE, (int)M, (const float*)tr->dpx,
                        P + bo.xk, (const float*)tr->zx[k * L + L - 1], tr->dA);
     Lc.check();
@@ -869,16 +950,14 @@ int ecnf_fm_loss_grad(ecnf_trainer* tr, const float* params, const float* x1, co
       hipLaunchKernelGGL(k_gate_bwd, dim3((unsigned)((BE + 3) / 4)), dim3(256), 0, s, G, m,
                          (const float*)tr->gate[k], (const float*)tr->dhcat, P + bo.gk, tr->dm_gate, tr->de);
       Lc.check();
-      Lc.gemm_wgrad((int)M, 1, (int)BE, m, M, tr->de, 1, dP + bo.gk, 1);
-      Lc.colsum(tr->de, (int)BE, 1, 1, dP + bo.gb);
+      Lc.gemm_wgrad((int)M, 1, (int)BE, m, M, tr->de, 1, dP + bo.gk, 1, dP + bo.gb);
     }
     // phi_x torso backward: layers L-1 .. 0; the input of layer 0 is m
     float* dZ = tr->dA;
     float* other = tr->dB;
     for (long l = L - 1; l >= 0; --l) {
       const float* X = l == 0 ? m : tr->ax[k * L + l - 1];
-      Lc.gemm_wgrad((int)M, (int)M, (int)BE, X, M, dZ, M, dP + bo.tk[l], M);
-      Lc.colsum(dZ, (int)BE, (int)M, M, dP + bo.tb[l]);
+      Lc.gemm_wgrad((int)M, (int)M, (int)BE, X, M, dZ, M, dP + bo.tk[l], M, dP + bo.tb[l]);
       if (l > 0) {
         Lc.gemm(false, true, (int)BE, (int)M, (int)M, dZ, M, P + bo.tk[l], M, other, M, nullptr, nullptr, 0,
                 tr->zx[k * L + l - 1], M);
@@ -891,8 +970,7 @@ int ecnf_fm_loss_grad(ecnf_trainer* tr, const float* params, const float* x1, co
     }
     // phi_e backward: layers L-1 .. 1 (layer 0 is the factorised layer 1)
     for (long l = L - 1; l >= 1; --l) {
-      Lc.gemm_wgrad((int)M, (int)M, (int)BE, tr->ae[k * L + l - 1], M, dZ, M, dP + bo.ek[l], M);
-      Lc.colsum(dZ, (int)BE, (int)M, M, dP + bo.eb[l]);
+      Lc.gemm_wgrad((int)M, (int)M, (int)BE, tr->ae[k * L + l - 1], M, dZ, M, dP + bo.ek[l], M, dP + bo.eb[l]);
       Lc.gemm(false, true, (int)BE, (int)M, (int)M, dZ, M, P + bo.ek[l], M, other, M, nullptr, nullptr, 0,
               tr->ze[k * L + l - 1], M);
       std::swap(dZ, other);
@@ -902,8 +980,7 @@ int ecnf_fm_loss_grad(ecnf_trainer* tr, const float* params, const float* x1, co
       // |r|^2 per edge into `other` (scratch), then dw_d = (|r|^2)^T dz1
       hipLaunchKernelGGL(k_square, dim3(nb(BE)), dim3(256), 0, s, BE, (const float*)tr->len[k], other);
       Lc.check();
-      Lc.gemm_wgrad(1, (int)M, (int)BE, other, 1, dZ, M, dP + bo.ek[0] + 2 * H * M, M);
-      Lc.colsum(dZ, (int)BE, (int)M, M, dP + bo.eb[0]);
+      Lc.gemm_wgrad(1, (int)M, (int)BE, other, 1, dZ, M, dP + bo.ek[0] + 2 * H * M, M, dP + bo.eb[0]);
       hipLaunchKernelGGL(k_layer1_node_bwd, dim3(nb(BN * M)), dim3(256), 0, s, G, (const float*)dZ, tr->dPs,
                          tr->dPr);
       Lc.check();
@@ -923,8 +1000,7 @@ int ecnf_fm_loss_grad(ecnf_trainer* tr, const float* params, const float* x1, co
     Lc.check();
     std::swap(dx, dxn);
     // node Dense: dWn = hin^T dh1, dbn, dhin = dh1 Wn^T
-    Lc.gemm_wgrad((int)(H + T), (int)H, (int)BN, tr->hin[k], H + T, tr->dh1, H, dP + bo.nk, H);
-    Lc.colsum(tr->dh1, (int)BN, (int)H, H, dP + bo.nb);
+    Lc.gemm_wgrad((int)(H + T), (int)H, (int)BN, tr->hin[k], H + T, tr->dh1, H, dP + bo.nk, H, dP + bo.nb);
     Lc.gemm(false, true, (int)BN, (int)(H + T), (int)H, tr->dh1, H, P + bo.nk, H, tr->dhin, H + T);
     dh_next = nullptr;
     if (k > 0) {
@@ -935,9 +1011,16 @@ int ecnf_fm_loss_grad(ecnf_trainer* tr, const float* params, const float* x1, co
       dh_next = tr->dhn;
     }
   }
-  hipLaunchKernelGGL(k_embed_bwd, dim3(nb((long)G.nfeat * H)), dim3(256), 0, s, G, (const float*)tr->dhin, H + T,
-                     feat, dP + o.emb);
-  Lc.check();
+  {
+    const unsigned chunks = (unsigned)((BN + 63) / 64), hc = (unsigned)((H + 63) / 64);
+    hipLaunchKernelGGL(k_embed_bwd, dim3((unsigned)G.nfeat * hc, chunks), dim3(256), 0, s, G, (const float*)tr->dhin,
+                       H + T, feat, tr->split);
+    Lc.check();
+    const long ne = (long)G.nfeat * H;
+    hipLaunchKernelGGL(reduce_splits, dim3(nb(ne)), dim3(256), 0, s, (const float*)tr->split, (int)chunks, ne,
+                       dP + o.emb, 0, (const float*)nullptr, 0L, (float*)nullptr);
+    Lc.check();
+  }
   if (Lc.err != hipSuccess) return fail(ECNF_E_HIP, std::string("training step launch: ") + hipGetErrorString(Lc.err));
   return ECNF_OK;
 }
@@ -956,7 +1039,7 @@ int ecnf_adam_update(ecnf_trainer* tr, const float* grad, float* params, float* 
                      o->eps, o->eps_root, bc1, bc2, o->ema_beta, tr->norm_part);
   TR_TRY(hipGetLastError());
   if (norms) {
-    hipLaunchKernelGGL(k_norms, dim3(1), dim3(64), 0, s, (int)nbk, (const float*)tr->norm_part, norms);
+    hipLaunchKernelGGL(k_norms, dim3(1), dim3(256), 0, s, (int)nbk, (const float*)tr->norm_part, norms);
     TR_TRY(hipGetLastError());
   }
   return ECNF_OK;
