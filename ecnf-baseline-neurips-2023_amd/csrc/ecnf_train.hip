@@ -24,6 +24,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdint>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -49,7 +50,7 @@ __device__ __forceinline__ float dsilu(float z) {
 // GEMM: C[M][N] = alpha op(A)[M][K] op(B)[K][N] (+ bias[N]) (+ R) (+ C if accumulate), then optionally
 // z *= silu'(Zs) (the backward of a SiLU layer) and Aout = silu(z) (the forward one, C keeps the pre-activation).
 // TA: A stored [K][M] (lda over m); TB: B stored [N][K].  ksplit > 1: block z sums its k-range into the partial
-// C + z * split_stride (no epilogue), combined by reduce_splits in split order.  colsum (weight gradients, TA && !TB):
+// C + z * split_stride (no epilogue), combined by reduce_batched in split order.  colsum (weight gradients, TA && !TB):
 // the column sums of B over the block's k-range (the bias gradient sum_k dZ[k][n]), written by the first m-tile's
 // wave 0 into colsum[n] (ksplit == 1) or colsum_part[z][n].
 //
@@ -71,12 +72,17 @@ struct GemmArgs {
   int accumulate;
   int ksplit; long split_stride;
   float* colsum; float* colsum_part;
+  int sqA;   // A's elements enter squared (|r|^2 from the edge lengths)
 };
 
 constexpr int GT = 64, GK = 32, GS = GK + 1, GE = GT * GK / 256;   // GE: elements per thread per operand tile
 
-template <bool TA, bool TB>
+template <bool TA, bool TB, bool VA, bool VB>
 __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
+  // VA / VB (host-checked for the whole launch): the operand's rows are 16-B aligned, its tiles whole (the m / n
+  // extent a multiple of 64, K a multiple of 32), so it is loaded as float4s; otherwise as clamped scalars (every lane
+  // loads a valid address, out-of-range elements are zeroed afterwards: no divergent branches around the loads, so
+  // the next tile's loads stay in flight across the MFMAs)
   __shared__ float As[2][GT * GS];
   __shared__ float Bs[2][GT * GS];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -88,7 +94,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
     kb = blockIdx.z * kc;
     ke = min(g.K, kb + kc);
   }
-  // element e of this thread's share: (row within the tile, k within the tile), source-coalesced
+  // scalar element e of this thread: (row within the tile, k within the tile), source-coalesced
   auto a_idx = [&](int e, int& mm, int& kk) {
     const int i = tid + 256 * e;
     if (TA) { mm = i % GT; kk = i / GT; } else { kk = i % GK; mm = i / GK; }
@@ -99,27 +105,78 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
   };
   float ra[GE], rb[GE];
   auto load = [&](int k0) {
+    if (VA) {
 #pragma unroll
-    for (int e = 0; e < GE; ++e) {
-      int mm, kk;
-      a_idx(e, mm, kk);
-      const int gm = m0 + mm, gk = k0 + kk;
-      ra[e] = (gm < g.M && gk < ke) ? (TA ? g.A[(long)gk * g.lda + gm] : g.A[(long)gm * g.lda + gk]) : 0.f;
-      int nn;
-      b_idx(e, nn, kk);
-      const int gn = n0 + nn, gk2 = k0 + kk;
-      rb[e] = (gn < g.N && gk2 < ke) ? (TB ? g.B[(long)gn * g.ldb + gk2] : g.B[(long)gk2 * g.ldb + gn]) : 0.f;
+      for (int e = 0; e < GE / 4; ++e) {
+        const int q = tid + 256 * e;
+        const float4 v = TA ? *reinterpret_cast<const float4*>(g.A + (long)(k0 + q / 16) * g.lda + m0 + 4 * (q % 16))
+                            : *reinterpret_cast<const float4*>(g.A + (long)(m0 + q / 8) * g.lda + k0 + 4 * (q % 8));
+        ra[4 * e] = v.x; ra[4 * e + 1] = v.y; ra[4 * e + 2] = v.z; ra[4 * e + 3] = v.w;
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < GE; ++e) {
+        int mm, kk;
+        a_idx(e, mm, kk);
+        const int gm = min(m0 + mm, g.M - 1), gk = min(k0 + kk, ke - 1);
+        ra[e] = TA ? g.A[(long)gk * g.lda + gm] : g.A[(long)gm * g.lda + gk];
+      }
+    }
+    if (VB) {
+#pragma unroll
+      for (int e = 0; e < GE / 4; ++e) {
+        const int q = tid + 256 * e;
+        const float4 v = TB ? *reinterpret_cast<const float4*>(g.B + (long)(n0 + q / 8) * g.ldb + k0 + 4 * (q % 8))
+                            : *reinterpret_cast<const float4*>(g.B + (long)(k0 + q / 16) * g.ldb + n0 + 4 * (q % 16));
+        rb[4 * e] = v.x; rb[4 * e + 1] = v.y; rb[4 * e + 2] = v.z; rb[4 * e + 3] = v.w;
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < GE; ++e) {
+        int nn, kk;
+        b_idx(e, nn, kk);
+        const int gn = min(n0 + nn, g.N - 1), gk = min(k0 + kk, ke - 1);
+        rb[e] = TB ? g.B[(long)gn * g.ldb + gk] : g.B[(long)gk * g.ldb + gn];
+      }
     }
   };
-  auto store = [&](int buf) {
+  auto store = [&](int buf, int k0) {
+    if (VA) {
 #pragma unroll
-    for (int e = 0; e < GE; ++e) {
-      int mm, kk;
-      a_idx(e, mm, kk);
-      As[buf][mm * GS + kk] = ra[e];
-      int nn;
-      b_idx(e, nn, kk);
-      Bs[buf][nn * GS + kk] = rb[e];
+      for (int e = 0; e < GE / 4; ++e) {
+        const int q = tid + 256 * e;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (TA) As[buf][(4 * (q % 16) + j) * GS + q / 16] = ra[4 * e + j];
+          else As[buf][(q / 8) * GS + 4 * (q % 8) + j] = ra[4 * e + j];
+        }
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < GE; ++e) {
+        int mm, kk;
+        a_idx(e, mm, kk);
+        const float v = g.sqA ? ra[e] * ra[e] : ra[e];
+        As[buf][mm * GS + kk] = (m0 + mm < g.M && k0 + kk < ke) ? v : 0.f;
+      }
+    }
+    if (VB) {
+#pragma unroll
+      for (int e = 0; e < GE / 4; ++e) {
+        const int q = tid + 256 * e;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (TB) Bs[buf][(q / 8) * GS + 4 * (q % 8) + j] = rb[4 * e + j];
+          else Bs[buf][(4 * (q % 16) + j) * GS + q / 16] = rb[4 * e + j];
+        }
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < GE; ++e) {
+        int nn, kk;
+        b_idx(e, nn, kk);
+        Bs[buf][nn * GS + kk] = (n0 + nn < g.N && k0 + kk < ke) ? rb[e] : 0.f;
+      }
     }
   };
   const bool do_colsum = g.colsum && blockIdx.y == 0 && tid < GT;
@@ -127,7 +184,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
   f32x16 acc = {};
   if (kb < ke) {
     load(kb);
-    store(0);
+    store(0, kb);
   }
   __syncthreads();
   int buf = 0;
@@ -136,13 +193,19 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
     if (more) load(k0 + GK);
     const float* Ab = &As[buf][(wm + (lane & 31)) * GS + (lane >> 5)];
     const float* Bb = &Bs[buf][(wn + (lane & 31)) * GS + (lane >> 5)];
+    float av[GK / 2], bv[GK / 2];
 #pragma unroll
-    for (int kk = 0; kk < GK; kk += 2) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(Ab[kk], Bb[kk], acc, 0, 0, 0);
+    for (int kk = 0; kk < GK / 2; ++kk) {
+      av[kk] = Ab[2 * kk];
+      bv[kk] = Bb[2 * kk];
+    }
+#pragma unroll
+    for (int kk = 0; kk < GK / 2; ++kk) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[kk], bv[kk], acc, 0, 0, 0);
     if (do_colsum) {
 #pragma unroll 8
       for (int kk = 0; kk < GK; ++kk) csum += Bs[buf][tid * GS + kk];
     }
-    if (more) store(buf ^ 1);
+    if (more) store(buf ^ 1, k0 + GK);
     __syncthreads();
     buf ^= 1;
   }
@@ -150,45 +213,82 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
     if (g.ksplit > 1) g.colsum_part[(long)blockIdx.z * g.N + n0 + tid] = csum;
     else g.colsum[n0 + tid] = csum;
   }
+  // epilogue: every operand of the 16 rows is loaded (clamped addresses) before any store, so the loads overlap
+  // (C may alias nothing the epilogue reads except itself under `accumulate`)
   const int col = n0 + wn + (lane & 31);
   if (col >= g.N) return;
+  int rows[16];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int row = m0 + wm + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-    if (row >= g.M) continue;
-    float z = g.alpha * acc[r];
-    if (g.ksplit > 1) {
-      g.C[blockIdx.z * g.split_stride + (long)row * g.ldc + col] = z;
-      continue;
-    }
-    if (g.bias) z += g.bias[col];
-    if (g.R) z += g.R[(long)row * g.ldr + col];
-    if (g.accumulate) z += g.C[(long)row * g.ldc + col];
-    if (g.Zs) z *= dsilu(g.Zs[(long)row * g.ldz + col]);
-    g.C[(long)row * g.ldc + col] = z;
-    if (g.Aout) g.Aout[(long)row * g.ldo + col] = silu(z);
+  for (int r = 0; r < 16; ++r) rows[r] = m0 + wm + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+  float z[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) z[r] = g.alpha * acc[r];
+  if (g.ksplit > 1) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+      if (rows[r] < g.M) g.C[blockIdx.z * g.split_stride + (long)rows[r] * g.ldc + col] = z[r];
+    return;
+  }
+  auto ld16 = [&](const float* p, long ld, float* out) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) out[r] = p[(long)min(rows[r], g.M - 1) * ld + col];
+  };
+  if (g.bias) {
+    const float b = g.bias[col];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) z[r] += b;
+  }
+  float t[16];
+  if (g.R) {
+    ld16(g.R, g.ldr, t);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) z[r] += t[r];
+  }
+  if (g.accumulate) {
+    ld16(g.C, g.ldc, t);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) z[r] += t[r];
+  }
+  if (g.Zs) {
+    ld16(g.Zs, g.ldz, t);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) z[r] *= dsilu(t[r]);
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r)
+    if (rows[r] < g.M) g.C[(long)rows[r] * g.ldc + col] = z[r];
+  if (g.Aout) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+      if (rows[r] < g.M) g.Aout[(long)rows[r] * g.ldo + col] = silu(z[r]);
   }
 }
 
-// dst[i] (+)= sum_s P[s][i], s in order; the n2 entries after the first n come from P2 [S][n2] into dst2 (the
-// column-sum partials of a weight-gradient GEMM reduced in the same launch)
-__global__ void reduce_splits(const float* __restrict__ P, int S, long n, float* dst, int accumulate,
-                              const float* __restrict__ P2, long n2, float* dst2) {
-  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n + n2) return;
-  const float* src = P;
-  float* out = dst;
-  long stride = n;
-  if (i >= n) {
-    i -= n;
-    src = P2;
-    out = dst2;
-    stride = n2;
-  }
+// Deferred split reductions: dst[i] = sum_s P[s][i] (s in order) for up to kRedMax (P, S, n, dst) entries in one
+// launch.  Nothing in the step reads a gradient before the step ends, so the weight-gradient GEMMs' partials stay in
+// a partial arena and are reduced together (one launch per arena fill instead of one per GEMM).  Entry e owns blocks
+// [first[e], first[e + 1]) of 256 outputs each.
+constexpr int kRedMax = 64;
+struct RedEntry {
+  const float* P;
+  float* dst;
+  int S, n, first;
+};
+struct RedBatch {
+  int count;
+  RedEntry e[kRedMax];
+};
+
+__global__ void reduce_batched(RedBatch rb) {
+  int k = 0;
+  while (k + 1 < rb.count && (int)blockIdx.x >= rb.e[k + 1].first) ++k;
+  const RedEntry& r = rb.e[k];
+  const long i = (long)((int)blockIdx.x - r.first) * blockDim.x + threadIdx.x;
+  if (i >= r.n) return;
   float acc = 0.f;
 #pragma unroll 4
-  for (int s = 0; s < S; ++s) acc += src[(long)s * stride + i];
-  out[i] = (accumulate && out == dst) ? out[i] + acc : acc;
+  for (int q = 0; q < r.S; ++q) acc += r.P[(long)q * r.n + i];
+  r.dst[i] = acc;
 }
 
 // ---------------------------------------------------------------------------------------------------------------
@@ -415,11 +515,6 @@ __global__ void k_copy_add(long rows, int cols, const float* __restrict__ X, lon
   out[r * ldo + c] = X[r * ldx + c] + (Y ? Y[r * ldy + c] : 0.0f);
 }
 
-__global__ void k_square(long n, const float* __restrict__ x, float* out) {
-  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) out[i] = x[i] * x[i];
-}
-
 // gate / aggregation backward (egnn.py:99-104): dm_i = dhcat[:, :M] of the receiver; per edge
 // dgm = dm_i / sqrt(N-1); de = (m . dgm) g (1 - g); dm = g dgm + de w_g.  64 threads per edge.
 __global__ void k_gate_bwd(Geom G, const float* __restrict__ m, const float* __restrict__ gate,
@@ -441,12 +536,17 @@ __global__ void k_gate_bwd(Geom G, const float* __restrict__ m, const float* __r
 
 // shift backward (egnn.py:87-95): with dD = d x_out[receiver] / (N - 1), den = C + |r|:
 //   dpx = dD . r / den;  dr = px dD / den - px (r . dD) / den^2 * d|r|/dr  (d|r|/dr = r / |r|, 0 for safe_norm's 1)
+// fused with the phi_x torso's last layer: dZ[e][c] = dpx w_x[c] silu'(Z[e][c]) (the Dense(1) output's input).
+// One thread per (edge, column); column 0 also writes dpx and dr
 __global__ void k_shift_bwd(Geom G, const float* __restrict__ dxout, const float* __restrict__ px,
-                            const float* __restrict__ r, const float* __restrict__ len, float* dpx, float* dr) {
-  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= (long)G.B * G.E) return;
+                            const float* __restrict__ r, const float* __restrict__ len, const float* __restrict__ wx,
+                            const float* __restrict__ Z, float* dpx, float* dr, float* dZ) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long)G.B * G.E * G.M) return;
+  const long e = idx / G.M;
+  const int c = (int)(idx - e * G.M);
   const long row = e / (G.N - 1);
-  const float l = len[e], den = G.C + l, p = px[e];
+  const float l = len[e], den = G.C + l;
   float x2 = 0.f, rd = 0.f, dD[3];
   for (int d = 0; d < G.D; ++d) {
     dD[d] = dxout[row * G.D + d] / (float)(G.N - 1);
@@ -454,19 +554,14 @@ __global__ void k_shift_bwd(Geom G, const float* __restrict__ dxout, const float
     x2 += rv * rv;
     rd += rv * dD[d];
   }
-  dpx[e] = rd / den;
-  const float dl = x2 == 0.f ? 0.f : -p * rd / (den * den) / l;
-  for (int d = 0; d < G.D; ++d) dr[e * G.D + d] = p * dD[d] / den + dl * r[e * G.D + d];
-}
-
-// dZ = (dpx w_x) * silu'(Z) for the phi_x torso's last layer (the Dense(1) output's input)
-__global__ void k_outer_dsilu(long rows, int M, const float* __restrict__ dpx, const float* __restrict__ w,
-                              const float* __restrict__ Z, float* dZ) {
-  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= rows * M) return;
-  const long e = idx / M;
-  const int c = (int)(idx - e * M);
-  dZ[idx] = dpx[e] * w[c] * dsilu(Z[idx]);
+  const float dp = rd / den;
+  dZ[idx] = dp * wx[c] * dsilu(Z[idx]);
+  if (c == 0) {
+    const float p = px[e];
+    dpx[e] = dp;
+    const float dl = x2 == 0.f ? 0.f : -p * rd / (den * den) / l;
+    for (int d = 0; d < G.D; ++d) dr[e * G.D + d] = p * dD[d] / den + dl * r[e * G.D + d];
+  }
 }
 
 // layer-1 backward, node side: dP_r[i] = sum over the receiver's edges of dz1, dP_s[j] = sum over the sender's
@@ -524,7 +619,7 @@ __global__ void k_dx_bwd(Geom G, const float* __restrict__ dxout, const float* _
 
 // embedding gradient: dEmb[f][c] = sum over node rows with feature f of dhin[row][c].  Partial sums over chunks of
 // 64 rows (256 threads = 4 row lanes x 64 columns; grid.x = n_features x column blocks, grid.y = row chunks), each
-// chunk's 4 lanes combined in order; the chunks are summed in order by reduce_splits: part[chunk][f H + c]
+// chunk's 4 lanes combined in order; the chunks are summed in order by reduce_batched: part[chunk][f H + c]
 __global__ void k_embed_bwd(Geom G, const float* __restrict__ dhin, long ld, const int32_t* __restrict__ feat,
                             float* part) {
   __shared__ float red[4][64];
@@ -676,8 +771,8 @@ struct ecnf_trainer {
   float *ut, *mean, *temb, *part_loss, *part_dfs, *dxa, *dxb, *norm_part;
   std::vector<float*> xc, hin, h1, Ps, Pr, r, len, px, gate, hcat;   // [K] (xc: [K + 1])
   std::vector<float*> ze, ae, zx, ax, zh, ah;                        // [K * L], [K * (L + 1)]
-  float *dA, *dB, *dm_gate, *de, *dpx, *dr, *dPs, *dPr, *dhcat, *dh1, *dhin, *dhA, *dhB, *dhn, *split, *csplit;
-  size_t split_floats, csplit_floats;
+  float *dA, *dB, *dm_gate, *de, *dpx, *dr, *dPs, *dPr, *dhcat, *dh1, *dhin, *dhA, *dhB, *dhn, *red;
+  size_t red_floats;   // partial arena of the deferred split reductions
 };
 
 namespace {
@@ -697,39 +792,82 @@ struct Launcher {
             long ldc, const float* bias = nullptr, const float* R = nullptr, long ldr = 0, const float* Zs = nullptr,
             long ldz = 0, float* Aout = nullptr, long ldo = 0, int accumulate = 0) {
     GemmArgs g{M, N, K, A, lda, B, ldb, C, ldc, 1.0f, bias, R, ldr, Zs, ldz, Aout, ldo, accumulate, 1, 0,
-               nullptr, nullptr};
+               nullptr, nullptr, 0};
     dim3 grid(nblk(N, GT), nblk(M, GT), 1);
     launch(ta, tb, g, grid);
   }
+  // deferred split reductions (reduce_batched)
+  std::vector<RedEntry> pending;
+  size_t red_used = 0;   // floats of tr->red in use by pending partials
+
+  float* red_alloc(size_t floats) {
+    if (red_used + floats > tr->red_floats) flush();
+    float* p = tr->red + red_used;
+    red_used += (floats + 63) & ~size_t(63);
+    return p;
+  }
+  void defer(const float* P, int S, long n, float* dst) {
+    pending.push_back(RedEntry{P, dst, S, (int)n, 0});
+  }
+  void flush() {
+    for (size_t b = 0; b < pending.size(); b += kRedMax) {
+      RedBatch rb{};
+      rb.count = (int)std::min<size_t>(kRedMax, pending.size() - b);
+      int blocks = 0;
+      for (int k = 0; k < rb.count; ++k) {
+        rb.e[k] = pending[b + k];
+        rb.e[k].first = blocks;
+        blocks += (int)nblk(rb.e[k].n);
+      }
+      hipLaunchKernelGGL(reduce_batched, dim3((unsigned)blocks), dim3(256), 0, s, rb);
+      check();
+    }
+    pending.clear();
+    red_used = 0;
+  }
+
   // weight gradient dW[M][N] = A^T dZ over K rows and the bias gradient db[N] = sum_k dZ[k] (db may be NULL),
-  // split over the K dimension into >= ~384 workgroups of >= 128 rows, reduced in split order in one launch
+  // split over the K dimension into >= ~384 workgroups of >= 128 rows; the partials are reduced (in split order) by
+  // the next flush().  sqA: A's entries enter squared.  ldw == N for every weight block of the flat blob.
   void gemm_wgrad(int M, int N, int K, const float* A, long lda, const float* dZ, long ldz, float* dW, long ldw,
-                  float* db = nullptr) {
+                  float* db = nullptr, int sqA = 0) {
     const long n = (long)M * N;
     const long tiles = (long)nblk(M, GT) * nblk(N, GT);
     int S = (int)std::min<long>({128, std::max<long>(1, (384 + tiles - 1) / tiles), std::max<long>(1, K / 128)});
-    while (S > 1 && ((long)S * n > (long)tr->split_floats || (long)S * N > (long)tr->csplit_floats)) --S;
+    while (S > 1 && (size_t)S * (n + N + 128) > tr->red_floats) --S;
     if (S == 1) {
       GemmArgs g{M, N, K, A, lda, dZ, ldz, dW, ldw, 1.0f, nullptr, nullptr, 0, nullptr, 0, nullptr, 0, 0, 1, 0,
-                 db, nullptr};
+                 db, nullptr, sqA};
       launch(true, false, g, dim3(nblk(N, GT), nblk(M, GT), 1));
       return;
     }
-    GemmArgs g{M, N, K, A, lda, dZ, ldz, tr->split, N, 1.0f, nullptr, nullptr, 0, nullptr, 0, nullptr, 0, 0, S, n,
-               db, tr->csplit};
+    float* P = red_alloc((size_t)S * n);
+    float* Pb = db ? red_alloc((size_t)S * N) : nullptr;
+    GemmArgs g{M, N, K, A, lda, dZ, ldz, P, N, 1.0f, nullptr, nullptr, 0, nullptr, 0, nullptr, 0, 0, S, n,
+               db, Pb, sqA};
     launch(true, false, g, dim3(nblk(N, GT), nblk(M, GT), S));
-    // ldw == N for every weight block of the flat blob (row-major [in][out])
-    const long n2 = db ? N : 0;
-    hipLaunchKernelGGL(reduce_splits, dim3(nblk(n + n2)), dim3(256), 0, s, tr->split, S, n, dW, 0,
-                       (const float*)tr->csplit, n2, db);
-    check();
+    defer(P, S, n, dW);
+    if (db) defer(Pb, S, N, db);
+  }
+  template <bool TA, bool TB>
+  void launch_t(const GemmArgs& g, dim3 grid) {
+    auto aligned = [](const float* p, long ld) {
+      return ((reinterpret_cast<uintptr_t>(p) | (uintptr_t)(ld * 4)) & 15) == 0;
+    };
+    const bool kw = g.K % GK == 0;
+    const bool va = kw && g.M % GT == 0 && aligned(g.A, g.lda) && !g.sqA;
+    const bool vb = kw && g.N % GT == 0 && aligned(g.B, g.ldb);
+    if (va && vb) hipLaunchKernelGGL((gemm_kernel<TA, TB, true, true>), grid, dim3(256), 0, s, g);
+    else if (va) hipLaunchKernelGGL((gemm_kernel<TA, TB, true, false>), grid, dim3(256), 0, s, g);
+    else if (vb) hipLaunchKernelGGL((gemm_kernel<TA, TB, false, true>), grid, dim3(256), 0, s, g);
+    else hipLaunchKernelGGL((gemm_kernel<TA, TB, false, false>), grid, dim3(256), 0, s, g);
   }
   void launch(bool ta, bool tb, const GemmArgs& g, dim3 grid) {
     if (g.M <= 0 || g.N <= 0) return;
-    if (ta && tb) hipLaunchKernelGGL((gemm_kernel<true, true>), grid, dim3(256), 0, s, g);
-    else if (ta) hipLaunchKernelGGL((gemm_kernel<true, false>), grid, dim3(256), 0, s, g);
-    else if (tb) hipLaunchKernelGGL((gemm_kernel<false, true>), grid, dim3(256), 0, s, g);
-    else hipLaunchKernelGGL((gemm_kernel<false, false>), grid, dim3(256), 0, s, g);
+    if (ta && tb) launch_t<true, true>(g, grid);
+    else if (ta) launch_t<true, false>(g, grid);
+    else if (tb) launch_t<false, true>(g, grid);
+    else launch_t<false, false>(g, grid);
     check();
   }
 };
@@ -784,13 +922,12 @@ int ecnf_trainer_create(const ecnf_cfg* cfg, int32_t max_batch, int device, ecnf
   add(&tr->dr, BE * D); add(&tr->dPs, BN * M); add(&tr->dPr, BN * M); add(&tr->dhcat, BN * (M + H));
   add(&tr->dh1, BN * H); add(&tr->dhin, BN * (H + T)); add(&tr->dhA, BN * M); add(&tr->dhB, BN * M);
   add(&tr->dhn, BN * H);
-  // split-K partials: up to 128 splits of the largest weight block ((M + H) x M, (H + T) x H or 2H x M), their
-  // column sums (bias gradients), and the embedding gradient's row-chunk partials
-  tr->split_floats = (size_t)std::max<long>(128 * std::max({(M + H) * M, (H + T) * H, 2 * H * M}),
-                                            ((BN + 63) / 64) * (long)c.n_features * H);
-  add(&tr->split, (long)tr->split_floats);
-  tr->csplit_floats = (size_t)(128 * std::max({M + H, H + T, M}));
-  add(&tr->csplit, (long)tr->csplit_floats);
+  // partial arena of the deferred split reductions: at least 128 splits of the largest weight block and its bias
+  // ((M + H) x M, (H + T) x H) and the embedding gradient's row-chunk partials; 32 M floats (128 MiB) when larger,
+  // which holds a whole LJ13 step's partials in about two flushes
+  tr->red_floats = (size_t)std::max<long>({128 * (std::max((M + H) * M, (H + T) * H) + std::max(M + H, H + T) + 256),
+                                           ((BN + 63) / 64) * (long)c.n_features * H + 64, 32L << 20});
+  add(&tr->red, (long)tr->red_floats);
   size_t total = 0;
   for (auto& q : plan) total += (size_t)q.second;
   tr->arena_floats = total;
@@ -936,15 +1073,13 @@ int ecnf_fm_loss_grad(ecnf_trainer* tr, const float* params, const float* x1, co
                          (const float*)(tr->dhcat + M), M + H, tr->dh1, H);
       Lc.check();
     }
-    // shifts: dpx, dr (egnn.py:87-95)
-    hipLaunchKernelGGL(k_shift_bwd, dim3(nb(BE)), dim3(256), 0, s, G, (const float*)dx, (const float*)tr->px[k],
-                       (const float*)tr->r[k], (const float*)tr->len[k], tr->dpx, tr->dr);
+    // shifts: dpx, dr (egnn.py:87-95) and the phi_x torso's last dZ = dpx w_x silu'(z)
+    hipLaunchKernelGGL(k_shift_bwd, dim3(nb(BE * M)), dim3(256), 0, s, G, (const float*)dx, (const float*)tr->px[k],
+                       (const float*)tr->r[k], (const float*)tr->len[k], P + bo.xk,
+                       (const float*)tr->zx[k * L + L - 1], tr->dpx, tr->dr, tr->dA);
     Lc.check();
-    // phi_x output Dense(1): dw_x = a_x[L-1]^T dpx, db_x = sum dpx; dZ_x[L-1] = dpx w_x silu'(z)
+    // phi_x output Dense(1): dw_x = a_x[L-1]^T dpx, db_x = sum dpx
     Lc.gemm_wgrad((int)M, 1, (int)BE, tr->ax[k * L + L - 1], M, tr->dpx, 1, dP + bo.xk, 1, dP + bo.xb);
-    hipLaunchKernelGGL(k_outer_dsilu, dim3(nb(BE * M)), dim3(256), 0, s, BE, (int)M, (const float*)tr->dpx,
-                       P + bo.xk, (const float*)tr->zx[k * L + L - 1], tr->dA);
-    Lc.check();
     // gate path (egnn.py:99-104) into dm_gate, its weights
     if (need_h) {
       hipLaunchKernelGGL(k_gate_bwd, dim3((unsigned)((BE + 3) / 4)), dim3(256), 0, s, G, m,
@@ -977,10 +1112,8 @@ int ecnf_fm_loss_grad(ecnf_trainer* tr, const float* params, const float* x1, co
     }
     // layer 1: dz1 = dZ.  dw_d = |r|^2 . dz1, db, node halves, |r|^2 -> dr
     {
-      // |r|^2 per edge into `other` (scratch), then dw_d = (|r|^2)^T dz1
-      hipLaunchKernelGGL(k_square, dim3(nb(BE)), dim3(256), 0, s, BE, (const float*)tr->len[k], other);
-      Lc.check();
-      Lc.gemm_wgrad(1, (int)M, (int)BE, other, 1, dZ, M, dP + bo.ek[0] + 2 * H * M, M, dP + bo.eb[0]);
+      // dw_d = (|r|^2)^T dz1 (the lengths squared as they are loaded)
+      Lc.gemm_wgrad(1, (int)M, (int)BE, tr->len[k], 1, dZ, M, dP + bo.ek[0] + 2 * H * M, M, dP + bo.eb[0], 1);
       hipLaunchKernelGGL(k_layer1_node_bwd, dim3(nb(BN * M)), dim3(256), 0, s, G, (const float*)dZ, tr->dPs,
                          tr->dPr);
       Lc.check();
@@ -1013,14 +1146,14 @@ int ecnf_fm_loss_grad(ecnf_trainer* tr, const float* params, const float* x1, co
   }
   {
     const unsigned chunks = (unsigned)((BN + 63) / 64), hc = (unsigned)((H + 63) / 64);
-    hipLaunchKernelGGL(k_embed_bwd, dim3((unsigned)G.nfeat * hc, chunks), dim3(256), 0, s, G, (const float*)tr->dhin,
-                       H + T, feat, tr->split);
-    Lc.check();
     const long ne = (long)G.nfeat * H;
-    hipLaunchKernelGGL(reduce_splits, dim3(nb(ne)), dim3(256), 0, s, (const float*)tr->split, (int)chunks, ne,
-                       dP + o.emb, 0, (const float*)nullptr, 0L, (float*)nullptr);
+    float* part = Lc.red_alloc((size_t)chunks * ne);
+    hipLaunchKernelGGL(k_embed_bwd, dim3((unsigned)G.nfeat * hc, chunks), dim3(256), 0, s, G, (const float*)tr->dhin,
+                       H + T, feat, part);
     Lc.check();
+    Lc.defer(part, (int)chunks, ne, dP + o.emb);
   }
+  Lc.flush();
   if (Lc.err != hipSuccess) return fail(ECNF_E_HIP, std::string("training step launch: ") + hipGetErrorString(Lc.err));
   return ECNF_OK;
 }
