@@ -210,10 +210,15 @@ namespace {
     if (e_ != hipSuccess) return fail(ECNF_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
   } while (0)
 
+// edge slots per receiver (Net::SR): the receiver runs packed back to back while a run fits one 32-edge tile
+// (N <= 33: a run touches at most two tiles); beyond that every run is padded to two whole tiles
+constexpr int kMaxNodes = 64;
+int edge_slots_per_receiver(int n_nodes) { return n_nodes - 1 <= 32 ? n_nodes - 1 : 64; }
+
 int check_cfg(const ecnf_cfg* c) {
   if (!c) return fail(ECNF_E_INVALID, "cfg is NULL");
-  if (c->n_nodes < 2 || c->n_nodes > 33)
-    return fail(ECNF_E_UNSUPPORTED, "n_nodes must be in [2, 33] (a receiver's N-1 edges must fit one 32-edge tile)");
+  if (c->n_nodes < 2 || c->n_nodes > kMaxNodes)
+    return fail(ECNF_E_UNSUPPORTED, "n_nodes must be in [2, 64] (a receiver's N-1 edges must fit two 32-edge tiles)");
   if (c->dim != 2 && c->dim != 3) return fail(ECNF_E_UNSUPPORTED, "dim must be 2 or 3");
   if (c->n_features < 1) return fail(ECNF_E_INVALID, "n_features must be >= 1");
   if (c->hidden < 32 || c->hidden % 32) return fail(ECNF_E_UNSUPPORTED, "hidden must be a multiple of 32");
@@ -431,7 +436,8 @@ void set_mpw(Net& n, const ecnf_cfg& c, int NT, int P, int mpw, int rp) {
   n.MPW = mpw;
   n.RP = rp;
   const bool vec = split_primal(c, NT, P);
-  n.cross = vec && (size_t)mpw * (n.EP / 32) * ld_node(M, 1, true) <= (size_t)rp * ld_node(H + T, 1, true) &&
+  n.cross = vec && n.SR == c.n_nodes - 1 &&
+            (size_t)mpw * (n.EP / 32) * ld_node(M, 1, true) <= (size_t)rp * ld_node(H + T, 1, true) &&
             n.EP / 32 <= kMaxTilesPerMol;
   n.ncross = 0;
   const int nn1 = c.n_nodes - 1;
@@ -445,7 +451,7 @@ void set_mpw(Net& n, const ecnf_cfg& c, int NT, int P, int mpw, int rp) {
 
 int choose_mpw(const ecnf_cfg& c, int NT, int P, int* mpw_out, size_t* lds_out, int* rp_out) {
   const int N = c.n_nodes, D = c.dim, H = c.hidden, T = c.time_embedding_dim, M = c.mlp_width;
-  const int E = N * (N - 1);
+  const int E = N * (N - 1), SR = edge_slots_per_receiver(N);
   // experiment builds only (tools/build_timing.sh DEVFLAGS): -DECNF_FORCE_MPW / -DECNF_FORCE_MPW_TANGENT
 #ifndef ECNF_FORCE_MPW
 #define ECNF_FORCE_MPW 0
@@ -467,7 +473,7 @@ int choose_mpw(const ecnf_cfg& c, int NT, int P, int* mpw_out, size_t* lds_out, 
                        solver_lds_floats(m, N * D);
     const size_t bytes = (size_t)floats * 4;
     if (bytes > 160 * 1024) break;
-    const int EP = 32 * ((E + 31) / 32);
+    const int EP = 32 * ((N * SR + 31) / 32);
     const int tiles = m * EP / 32;
     const double eff = (double)tiles / (kSimds * ((tiles + kSimds - 1) / kSimds)) * (double)(m * E) / (tiles * 32.0);
     if (forced ? m == forced : eff > best + 1e-9) {
@@ -596,9 +602,21 @@ hipError_t dispatch_vf(const ecnf_handle* h, int NT, const float* x, const float
 bool exact_sparse(const ecnf_handle* h, int divergence) {
   const ecnf_cfg& c = h->cfg;
   if (divergence != ECNF_DIV_EXACT || h->prec != ECNF_PREC_SPLIT_F16 || c.mlp_width > 128) return false;
+  if (edge_slots_per_receiver(c.n_nodes) != c.n_nodes - 1) return false;   // receiver-tiled (N > 33): all-dual form
   if (c.mlp_depth == 2 && (c.mlp_width == 128 || c.dim == 2)) return false;
   const int nn1 = c.n_nodes - 1, tpm = (c.n_nodes * nn1 + 31) / 32, ndt = (2 * nn1 + 31) / 32;
   return tpm >= 3 * ndt;
+}
+
+// why a handle has no tangent (divergence / JVP) kernel: the shape is not compiled for it at this precision, or its
+// node rows (doubled by the tangent rows) do not fit the LDS of one CU (mlp_width 128 beyond 33 atoms, 256 beyond 32)
+std::string no_tangent_msg(const ecnf_cfg& c, int prec) {
+  const int P = prec == ECNF_PREC_FP32 ? 1 : 0;
+  if (!shape_supported(c, 1, P))
+    return "no tangent kernel for mlp_width=" + std::to_string(c.mlp_width) + ", mlp_depth=" + std::to_string(c.mlp_depth) +
+           " at this precision";
+  return "the tangent kernel's LDS does not fit one CU for n_nodes=" + std::to_string(c.n_nodes) +
+         ", mlp_width=" + std::to_string(c.mlp_width);
 }
 
 // floats of one molecule slot of the primal-aggregate cache: block 1's message sums [N][M] and the shift sums of
@@ -903,7 +921,8 @@ int ecnf_create(const ecnf_cfg* cfg, const float* params, size_t n_floats, int d
     std::memset(&n, 0, sizeof(Net));
     n.N = c.n_nodes; n.D = c.dim; n.H = H; n.T = T; n.M = M; n.L = L; n.K = K; n.nfeat = c.n_features;
     n.E = c.n_nodes * (c.n_nodes - 1);
-    n.EP = 32 * ((n.E + 31) / 32);
+    n.SR = edge_slots_per_receiver(c.n_nodes);
+    n.EP = 32 * ((c.n_nodes * n.SR + 31) / 32);
     n.ND = c.n_nodes * c.dim;
     n.C = c.normalization_constant;
     n.fs = fs;
@@ -1048,7 +1067,7 @@ int ecnf_vf_jvp(ecnf_handle* h, const float* x, const float* t, const int32_t* f
   if (batch < 0 || n_tangents < 1) return fail(ECNF_E_INVALID, "batch < 0 or n_tangents < 1");
   if (batch > 0 && (!x || !t || !feat || !tan_in || !tan_out)) return fail(ECNF_E_INVALID, "NULL argument");
   if (h->net[2 * h->prec + 1].MPW == 0)
-    return fail(ECNF_E_UNSUPPORTED, "no tangent kernel for mlp_width=" + std::to_string(h->cfg.mlp_width));
+    return fail(ECNF_E_UNSUPPORTED, no_tangent_msg(h->cfg, h->prec));
   if (batch == 0) return ECNF_OK;
   HIP_TRY(hipSetDevice(h->device));
   HIP_TRY(dispatch_vf(h, 1, x, t, feat, tan_in, n_tangents, v, tan_out, batch, (hipStream_t)stream));
@@ -1126,7 +1145,7 @@ int integrate_impl(ecnf_handle* h, const ecnf_solve_opts* o, const float* y0, co
   if (o->max_steps < 1) return fail(ECNF_E_INVALID, "max_steps < 1");
   const int NT = o->divergence == ECNF_DIV_NONE ? 0 : 1;
   if (NT && h->net[2 * h->prec + 1].MPW == 0)
-    return fail(ECNF_E_UNSUPPORTED, "no tangent kernel for mlp_width=" + std::to_string(h->cfg.mlp_width));
+    return fail(ECNF_E_UNSUPPORTED, no_tangent_msg(h->cfg, h->prec));
   if (batch == 0) return ECNF_OK;
   SolveP sp;
   sp.solver = o->solver;

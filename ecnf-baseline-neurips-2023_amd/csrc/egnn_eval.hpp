@@ -12,7 +12,8 @@
 //     Y^T[j][n] = sum_k W[k][j] X^T[k][n]: A = weights (global, L2-resident), B = node rows (LDS), one output
 //     32x32 tile per (32-output block, 32-node tile); the tangent tile shares every A fragment.
 //   * edge MLPs: edge e (receiver-major, graph.py:6-14) of a molecule sits on MFMA column (lane & 31) of a
-//     32-edge tile; a molecule owns EP = 32*ceil(N(N-1)/32) edge slots starting on a tile boundary.  A whole tile's activation is 16*M/32 registers per lane
+//     32-edge tile; a molecule owns EP = 32*ceil(N*SR/32) edge slots starting on a tile boundary (SR = N-1 slots
+//     per receiver for N <= 33; for 33 < N <= 64 every receiver run is padded to SR = 64 slots, two whole tiles).  A whole tile's activation is 16*M/32 registers per lane
 //     and the MFMA accumulator of layer l IS the B operand of layer l+1 (register r of output block fb is the
 //     k-step (fb, r)), so phi_e layers 2..L and all phi_x layers chain with zero LDS traffic; weights are
 //     pre-packed on the host into lane order (one dwordx4 per lane = 4 A fragments).
@@ -20,7 +21,8 @@
 //     halves are one node GEMM into LDS and are gathered per edge.
 //   * segment sums (e3nn.scatter_sum over the contiguous receiver runs) are segmented prefix scans in DPP
 //     (row_shr / row_bcast:15) inside each 32-edge tile followed by one LDS add per (segment, tile); a node's
-//     N-1 <= 32 edges touch at most two tiles and 0 + a + b == 0 + b + a, so the result is run-to-run deterministic.
+//     edges touch at most two tiles (N-1 <= 32 packed, or SR = 64 receiver-tiled) and 0 + a + b == 0 + b + a, so the
+//     result is run-to-run deterministic.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -158,7 +160,9 @@ struct BlockW {
 struct Net {
   int N, D, H, T, M, L, K, nfeat;
   int E;          // N (N - 1)
-  int EP;         // edges per molecule padded to a multiple of 32 (every molecule starts on a tile boundary)
+  int SR;         // edge slots per receiver: N - 1 (receiver runs packed back to back, N <= 33), or 64 (N > 33:
+                  // receiver-tiled, every run starts on a tile boundary and spans exactly two tiles)
+  int EP;         // edge slots per molecule (N SR) padded to a multiple of 32 (every molecule starts on a tile boundary)
   int MPW;        // molecules per workgroup
   int lds_floats; // dynamic LDS of one workgroup (device-checked build: ECNF_DCHECK bit 0)
   int RP;         // padded primal node rows
@@ -1115,7 +1119,7 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
     return;
   }
 #endif
-  const int N = net.N, E = net.E, nn1 = N - 1, RP = net.RP, M = NF * 32;
+  const int N = net.N, nn1 = N - 1, RP = net.RP, M = NF * 32;
   int mol, i, sd;
   bool valid;
   if (a < 0) {
@@ -1123,10 +1127,10 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
     // depend on which slot of the workgroup, i.e. which batch position, it occupies
     mol = (tile * 32) / net.EP;
     const int e_in = tile * 32 + li - mol * net.EP;
-    valid = (mol < net.MPW) && (e_in < E);
-    const int el = valid ? e_in : 0;
-    i = el / nn1;
-    sd = i + 1 + (el - i * nn1);
+    const int i0 = e_in / net.SR, j0 = e_in - i0 * net.SR;   // receiver, slot (receiver-tiled: j0 >= N - 1 is padding)
+    valid = (mol < net.MPW) && (i0 < N) && (j0 < nn1);
+    i = valid ? i0 : 0;
+    sd = i + 1 + (valid ? j0 : 0);
     if (sd >= N) sd -= N;
   } else {
     ECNF_DCHECK((Geo<NF, NT, P>::kL2T && tile < net.MPW && a < N), 6);

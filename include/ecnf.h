@@ -67,7 +67,7 @@ enum ecnf_divergence { ECNF_DIV_NONE = 0, ECNF_DIV_HUTCHINSON = 1, ECNF_DIV_EXAC
 /* Model hyper-parameters: the `flow:` block of examples/config/{dw4,lj13,aldp,qm9}.yaml and the
  * build_cnf(...) arguments (build_cnf.py:34-44).  mlp_units is (mlp_width,) * mlp_depth. */
 typedef struct ecnf_cfg {
-  int32_t n_nodes;             /* n_frames (N)                                   */
+  int32_t n_nodes;             /* n_frames (N), 2 .. 64                          */
   int32_t dim;                 /* spatial dim (D): 2 or 3                        */
   int32_t n_features;          /* nn.Embed vocabulary                            */
   int32_t hidden;              /* n_invariant_feat_hidden (H): multiple of 32    */

@@ -6,7 +6,8 @@ parts, molecule slots).  A child process runs every LJ13 mode through that libra
 batch-aware workgroup sizing (1, 5, 13, 300, 1024 molecules; the exact trace at every size, so the bounds of its
 primal-aggregate cache slots are checked at 1024 molecules too, bit 6) and reads the failed-check bits with
 ecnf_debug_checks(); they must be 0, and the outputs must match the product library (the checks do not touch the
-arithmetic)."""
+arithmetic).  A 48-atom molecule with the LJ13 widths runs the receiver-tiled edge layout (N > 33) through the same
+checks (field and Euler sample at 1, 7 and 300 molecules)."""
 import json
 import os
 import subprocess
@@ -50,6 +51,17 @@ for B in (1, 5, 13, 300, 1024):
     ye, dle, _, _ = h.integrate(x0, feat, 1.0, 0.0, SolveOptions("euler", 0.5), _lib.DIV_EXACT)
     rec = dict(z=z, v=v, ju=ju, y=y, yh=yh, dl=dl, ya=ya, ye=ye, dle=dle)
     out[B] = {k: w.detach().cpu().numpy() for k, w in rec.items()}
+# receiver-tiled edges (N = 48 > 33: every receiver's 47 edges on two whole tiles), the LJ13 widths: primal paths
+from ecnf_amd.params import CNFConfig
+big = CNFConfig(n_nodes=48, dim=3, n_features=1, hidden=64, mlp_width=128, mlp_depth=3, n_blocks=2, base_scale=1.0,
+                sigma_min=0.01)
+hb = EcnfHandle(big, init_params(big, 1), 0)
+for B in (1, 7, 300):
+    x0 = hb.base_sample(torch.randn((B, big.event_dim), device="cuda", generator=g))
+    feat = torch.zeros((B, big.n_nodes), device="cuda", dtype=torch.int32)
+    v = hb.vector_field(x0, torch.linspace(0.05, 0.95, B, device="cuda"), feat)
+    y, _, _, _ = hb.integrate(x0, feat, 0.0, 1.0, SolveOptions("euler", 0.25))
+    assert bool(torch.isfinite(v).all()) and bool(torch.isfinite(y).all())
 lib.ecnf_debug_checks(ctypes.byref(flags), 1)
 np.savez(sys.argv[1], **{f"{B}_{k}": w for B, d in out.items() for k, w in d.items()})
 print(json.dumps({"flags": int(flags.value)}))
