@@ -1,6 +1,7 @@
-"""A/B timing of tools/libt_*.so (tools/build_timing.sh): LJ13 B=1024 Euler NFE=100 integrate launches, each
-library in its own subprocess, ROUNDS interleaved rounds (A B C A B C ...) so clock drift hits all alike.
-Prints the median ms per launch of each library."""
+"""A/B timing of tools/libt_*.so (tools/build_timing.sh): integrate launches of one workload (default LJ13 B=1024
+Euler NFE=100; TV_CASE=aldp_sample / aldp_hutch / lj13_hutch select ALDP B=512 PID sample, ALDP B=512 PID
+Hutchinson log_prob, LJ13 B=1024 Euler Hutchinson), each library in its own subprocess, ROUNDS interleaved rounds
+(A B C A B C ...) so clock drift hits all alike.  Prints the median ms per launch of each library."""
 import glob
 import json
 import os
@@ -13,17 +14,23 @@ import os, sys, json, torch
 sys.path.insert(0, os.path.join(%r, "ecnf-baseline-neurips-2023_amd"))
 from ecnf_amd import CONFIGS, init_params
 from ecnf_amd.engine import EcnfHandle, SolveOptions
-cfg = CONFIGS["lj13"]
+from ecnf_amd import _lib
+case = os.environ.get("TV_CASE", "lj13")
+name, B = ("aldp", 512) if case.startswith("aldp") else ("lj13", 1024)
+cfg = CONFIGS[name]
 h = EcnfHandle(cfg, init_params(cfg, 0), 0)
-z = torch.randn((1024, cfg.event_dim), device="cuda", generator=torch.Generator("cuda").manual_seed(0))
+z = torch.randn((B, cfg.event_dim), device="cuda", generator=torch.Generator("cuda").manual_seed(0))
 x0 = h.base_sample(z)
-feat = torch.zeros((1024, cfg.n_nodes), device="cuda", dtype=torch.int32)
-o = SolveOptions("euler", 0.01)
-for _ in range(2): h.integrate(x0, feat, 0.0, 1.0, o, check_status=False)
+feat = (torch.arange(cfg.n_nodes, device="cuda", dtype=torch.int32).remainder(cfg.n_features)).expand(B, -1).contiguous()
+o = SolveOptions("euler", 0.01) if name == "lj13" else SolveOptions("dopri5", None)
+div = _lib.DIV_HUTCHINSON if case.endswith("hutch") else _lib.DIV_NONE
+t0, t1 = (1.0, 0.0) if case == "aldp_hutch" else (0.0, 1.0)
+eps = z if div else None
+for _ in range(2): h.integrate(x0, feat, t0, t1, o, div, eps, check_status=False)
 ts = []
 for _ in range(5):
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    a.record(); y = h.integrate(x0, feat, 0.0, 1.0, o, check_status=False)[0]; b.record(); torch.cuda.synchronize()
+    a.record(); y = h.integrate(x0, feat, t0, t1, o, div, eps, check_status=False)[0]; b.record(); torch.cuda.synchronize()
     ts.append(a.elapsed_time(b))
 print(json.dumps({"ms": sorted(ts)[2], "sum": float(y.double().abs().sum())}))
 """ % ROOT
