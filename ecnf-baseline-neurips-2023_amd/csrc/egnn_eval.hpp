@@ -1303,6 +1303,7 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
     // (staged in vecs), the aggregate's -ln2 / sqrt(N-1) in the split phi_h.0 weights, phi_x fed the messages as is
     edge_tail<NF, NT, L, D>(net, bw, s, X, XT, valid, rr, agg_dst, r, dr, length, dlength, lane, agg,
                             [&](f32x16 (&Y)[NF], f32x16 (&YT)[NF]) {
+                              STAMP_LANE0(s, kStEdgeAgg, t_sub);
                               const unsigned* Wx =
                                   launder_uniform(bw.Ws3 + (size_t)(L - 1) * SplitPlan<NF, 1>::GL * 3 * 256);
                               static_for<NF>([&](auto Fc) {
@@ -1313,8 +1314,10 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
                                   put_pair<NF, fb, 2 * i>(XAT, YT[fb][2 * i], YT[fb][2 * i + 1]);
                                 });
                               });
+                              STAMP_LANE0(s, kStEdgePhiXIn, t_sub);
                               chain_split<NF, L, 1, 3>(XA, XB, Y, Wx, s.vecs + (L - 1) * NF * 32, ix, lane, XAT, XBT,
                                                        YT);
+                              STAMP_LANE0(s, kStEdgePhiX, t_sub);
                             },
                             a < 0);   // block-1 dual tiles of the exact trace store tangents only
     STAMP_LANE0(s, kStEdgeTail, t_sub);
