@@ -82,7 +82,7 @@ def test_param_count_agrees(lib, name):
 @pytest.mark.parametrize("over,code", [
     (dict(mlp_width=96), _lib.ECNF_E_UNSUPPORTED),
     (dict(n_nodes=1), _lib.ECNF_E_UNSUPPORTED),
-    (dict(n_nodes=40), _lib.ECNF_E_UNSUPPORTED),
+    (dict(n_nodes=65), _lib.ECNF_E_UNSUPPORTED),
     (dict(dim=4), _lib.ECNF_E_UNSUPPORTED),
     (dict(hidden=48), _lib.ECNF_E_UNSUPPORTED),
     (dict(time_embedding_dim=7), _lib.ECNF_E_UNSUPPORTED),
