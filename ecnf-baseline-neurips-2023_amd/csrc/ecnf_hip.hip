@@ -28,7 +28,7 @@ namespace ecnf {
   ECNF_INST_SHAPE(ECNF_INST_KW, m, l, d, 0, 0) ECNF_INST_SHAPE(ECNF_INST_KW, m, l, d, 0, 1)
 #define ECNF_INST_BOTH(m, l, d) \
   ECNF_INST_PRIMAL(m, l, d) ECNF_INST_SHAPE(ECNF_INST_KW, m, l, d, 1, 0) ECNF_INST_SHAPE(ECNF_INST_KW, m, l, d, 1, 1)
-#define ECNF_INST_WIDE(m, l, d) ECNF_INST_PRIMAL(m, l, d) ECNF_INST_SHAPE(ECNF_INST_KW, m, l, d, 1, 0)
+#define ECNF_INST_WIDE(m, l, d) ECNF_INST_BOTH(m, l, d)
 #ifdef ECNF_SPLIT_TU
 #define ECNF_INST_KW extern template
 #else
@@ -408,15 +408,15 @@ bool split_primal(const ecnf_cfg& c, int NT, int P) {
   return kSplitChain && P == 0 && !NT && c.mlp_width <= 32 * kSplitMaxNF;
 }
 
-// Geo<NF, 1, 0>::kWideT: the M = 256 tangent kernels (per-edge phi_e.0, no P rows in LDS, in-place phi_h for one
-// 32-row node tile)
-bool wide_tangent(const ecnf_cfg& c, int NT, int P) { return NT && P == 0 && c.mlp_width == 256; }
+// Geo<NF, 1, P>::kWideT / kWideT32: the M = 256 tangent kernels at either precision (per-edge phi_e.0, no P rows in
+// LDS, in-place phi_h for one 32-row node tile)
+bool wide_tangent(const ecnf_cfg& c, int NT, int P) { (void)P; return NT && c.mlp_width == 256; }
 
 // Geo<NF, NT, P>::kSplitN: split node GEMMs, i.e. 16-B node-row strides (split primal kernels and, with
 // kSplitTanNode, the split tangent kernels)
 bool vec_layout(const ecnf_cfg& c, int NT, int P) {
   return split_primal(c, NT, P) || (kSplitTanNode && kSplitTanChain && P == 0 && NT && c.mlp_width <= 128) ||
-         wide_tangent(c, NT, P);
+         (P == 0 && wide_tangent(c, NT, P));
 }
 
 // dynamic LDS bytes of one workgroup holding m molecules (RP padded node rows)
@@ -493,13 +493,15 @@ int choose_mpw(const ecnf_cfg& c, int NT, int P, int* mpw_out, size_t* lds_out, 
 
 // a kernel is compiled for (cfg, NT, P); P < 0: either precision
 bool shape_supported(const ecnf_cfg& c, int NT, int P = -1) {
+  (void)NT;   // every compiled shape has tangent kernels at both precisions
+  (void)P;
   const int M = c.mlp_width, L = c.mlp_depth, D = c.dim;
 #define X(m, l, d) \
   if (M == m && L == l && D == d) return true;
   ECNF_SHAPES(X)
 #undef X
 #define X(m, l, d) \
-  if (M == m && L == l && D == d) return !NT || P <= 0;
+  if (M == m && L == l && D == d) return true;
   ECNF_SHAPES_WIDE_TAN(X)
 #undef X
   return false;
@@ -568,7 +570,7 @@ hipError_t dispatch_integrate(const ecnf_handle* h, int NT, const SolveP& sp, co
 #undef X
 #define X(m, l, d)                                                                                            \
   if (M == m && L == l && D == d)                                                                             \
-    return NT ? (P ? hipErrorInvalidValue : ECNF_CALL(m, l, d, 1, 0)) : (P ? ECNF_CALL(m, l, d, 0, 1) : ECNF_CALL(m, l, d, 0, 0));
+    return NT ? (P ? ECNF_CALL(m, l, d, 1, 1) : ECNF_CALL(m, l, d, 1, 0)) : (P ? ECNF_CALL(m, l, d, 0, 1) : ECNF_CALL(m, l, d, 0, 0));
   ECNF_SHAPES_WIDE_TAN(X)
 #undef X
 #undef ECNF_CALL
@@ -589,7 +591,7 @@ hipError_t dispatch_vf(const ecnf_handle* h, int NT, const float* x, const float
 #undef X
 #define X(m, l, d)                                                                                            \
   if (M == m && L == l && D == d)                                                                             \
-    return NT ? (P ? hipErrorInvalidValue : ECNF_CALL(m, l, d, 1, 0)) : (P ? ECNF_CALL(m, l, d, 0, 1) : ECNF_CALL(m, l, d, 0, 0));
+    return NT ? (P ? ECNF_CALL(m, l, d, 1, 1) : ECNF_CALL(m, l, d, 1, 0)) : (P ? ECNF_CALL(m, l, d, 0, 1) : ECNF_CALL(m, l, d, 0, 0));
   ECNF_SHAPES_WIDE_TAN(X)
 #undef X
 #undef ECNF_CALL
@@ -1040,7 +1042,7 @@ int ecnf_chain_arithmetic(ecnf_handle* h, int32_t with_tangent, int32_t* mode) {
   if (!h || !mode) return fail(ECNF_E_INVALID, "NULL argument");
   const bool split = split_primal(h->cfg, with_tangent ? 1 : 0, h->prec) ||
                      (kSplitTanChain && h->prec == ECNF_PREC_SPLIT_F16 && with_tangent && h->cfg.mlp_width <= 128) ||
-                     (kSplitTanChain && wide_tangent(h->cfg, with_tangent ? 1 : 0, h->prec));
+                     (kSplitTanChain && h->prec == ECNF_PREC_SPLIT_F16 && wide_tangent(h->cfg, with_tangent ? 1 : 0, h->prec));
 #ifdef ECNF_SPLIT_BF16
   *mode = split ? ECNF_CHAIN_SPLIT_BF16 : ECNF_CHAIN_FP32_MFMA;
 #else

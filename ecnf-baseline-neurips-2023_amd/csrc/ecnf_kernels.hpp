@@ -166,7 +166,7 @@ __global__ __launch_bounds__((Geo<NF, NT, P>::NTHR)) __attribute__((amdgpu_waves
   constexpr int kThreads = Geo<NF, NT, P>::NTHR;
   extern __shared__ float smem[];
   const int tid = threadIdx.x, MPW = net.MPW, ND = net.ND, N = net.N;
-  const Lds s = carve_lds<NT, Geo<NF, NT, P>::kSplitN, Geo<NF, NT, P>::kWideT>(net, smem);
+  const Lds s = carve_lds<NT, Geo<NF, NT, P>::kSplitN, Geo<NF, NT, P>::kNoP>(net, smem);
   const SolverLds st = carve_solver(s.tail, MPW, ND);
   const int mol0 = blockIdx.x * MPW;
   const int nmol = min(MPW, B - mol0);
@@ -418,7 +418,7 @@ __global__ __launch_bounds__((Geo<NF, NT, P>::NTHR)) __attribute__((amdgpu_waves
   constexpr int kThreads = Geo<NF, NT, P>::NTHR;
   extern __shared__ float smem[];
   const int tid = threadIdx.x, MPW = net.MPW, ND = net.ND, N = net.N;
-  const Lds s = carve_lds<NT, Geo<NF, NT, P>::kSplitN, Geo<NF, NT, P>::kWideT>(net, smem);
+  const Lds s = carve_lds<NT, Geo<NF, NT, P>::kSplitN, Geo<NF, NT, P>::kNoP>(net, smem);
   const SolverLds st = carve_solver(s.tail, MPW, ND);
   const int mol0 = blockIdx.x * MPW;
   const int nmol = min(MPW, B - mol0);
@@ -483,9 +483,9 @@ hipError_t launch_vf(const Net& net, size_t lds, const float* x, const float* t,
 
 // compiled shapes: (M, L, D) with tangent support where registers allow (M <= 128).  __graft_entry__.build()
 // reads these two lists to compile one ecnf_part.hip translation unit per shape.
-// ECNF_SHAPES: primal and tangent kernels in both GEMM arithmetics; ECNF_SHAPES_WIDE_TAN (M = 256): primal kernels in
-// both, tangent kernels in split fp16 only (Geo::kWideT; the strict-fp32 tangent chain needs 4 x 128 accumulator
-// registers per tile beside its inputs)
+// ECNF_SHAPES: primal and tangent kernels in both GEMM arithmetics; ECNF_SHAPES_WIDE_TAN (M = 256): the same, the
+// tangent kernels with per-edge phi_e.0 and sequential primal / tangent chain passes (Geo::kWideT split fp16,
+// Geo::kWideT32 strict fp32)
 #ifdef ECNF_DEV_LJ13_ONLY   // experiment builds (tools/build_variants.sh): the LJ13 shape only
 #define ECNF_SHAPES(X) X(128, 3, 3)
 #define ECNF_SHAPES_WIDE_TAN(X)

@@ -76,6 +76,11 @@ struct Geo {
   // M = 256 tangent kernels (QM9): per-edge phi_e.0 (no P buffer), sequential primal / tangent split chains
   // (chain_dual_seq), phi_h in place on macc
   static constexpr bool kWideT = kSplitTanChain && P == 0 && NT == 1 && NF == 8;
+  // M = 256 strict-fp32 tangent kernels (P = 1): kWideT's structure on v_mfma_f32_32x32x2_f32 (per-edge phi_e.0
+  // from the fp32 kernel rows, sequential primal / tangent chain passes, in-place phi_h): the fallback for QM9
+  // divergence solves whose activations leave the fp16 range and for checkpoints with edge weights >= 2^15
+  static constexpr bool kWideT32 = P == 1 && NT == 1 && NF == 8;
+  static constexpr bool kNoP = kWideT || kWideT32;   // no per-node phi_e.0 halves (P rows) in LDS
   static constexpr bool kSplitN = kSplit || (kSplitTanNode && kSplitT) || kWideT;
   // M <= 128 split tangent kernels: P (primal and tangent rows) in the log2 domain (the primal kernels' -log2(e)
   // fragments), phi_e.0's SiLU and its tangent evaluated there and split straight into the chain's input buffers
@@ -684,6 +689,35 @@ __device__ __forceinline__ void node_gemm_inplace(const float* X1, int ldx1, int
                                active ? 2 * wave : 0, 0, lane, active);
 }
 
+// the same in strict fp32 (the M = 256 fp32 tangent kernels, Geo::kWideT32): node_task's k-loop and epilogue on
+// v_mfma_f32_32x32x2_f32 with the epilogue behind a barrier every wave of the workgroup reaches
+template <int NT, int NW>
+__device__ __forceinline__ void node_gemm_inplace_f32(const float* X1, int ldx1, int K1, const float* X2, int ldx2,
+                                                      int K2, const float* __restrict__ W, int ldw,
+                                                      const float* __restrict__ bias, int NOUT, bool act, float* Y,
+                                                      int ldy, int RP, int nvalid, int wave, int lane) {
+  const int npair = NOUT >> 6;
+  const bool active = wave < npair;
+  const int jb = active ? 2 * wave : 0;
+  const int kk = lane >> 5, li = lane & 31;
+  ECNF_DCHECK(!active || RP == 32, 3);
+  f32x16 acc[2], accT[2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+    init_bias(acc[a], bias, jb + a, kk);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) accT[a][r] = 0.f;
+  }
+  if (active) {
+    const gfloat_p wcol = gptr(W) + kk * ldw + jb * 32 + li;
+    node_kloop<NT, 2>(acc, accT, wcol, ldw, X1 + li * ldx1 + kk, X1 + (RP + li) * ldx1 + kk, K1);
+    if (K2 > 0)
+      node_kloop<NT, 2>(acc, accT, wcol + K1 * ldw, ldw, X2 + li * ldx2 + kk, X2 + (RP + li) * ldx2 + kk, K2);
+  }
+  __syncthreads();
+  if (active) node_epilogue<NT, 2>(acc, accT, act, nullptr, 0, Y, ldy, RP, nvalid, jb, li, kk);
+}
+
 // ---------------------------------------------------------------------------------------------------
 // edge-MLP chain layer: b = silu(a W + bias), all in registers (a, b: NF blocks of 32 rows x 32 edges).
 // The A fragments of one (output block jb, input block fb) group are 4 dwordx4 per lane (16 MFMAs); groups are
@@ -1088,6 +1122,129 @@ __device__ __forceinline__ void edge_layer1_dual(const Net& net, const BlockW& b
     }
 }
 
+// ---------------------------------------------------------------------------------------------------
+// M = 256 strict-fp32 tangent kernels (Geo::kWideT32): the kWideT edge path on v_mfma_f32_32x32x2_f32.
+// ---------------------------------------------------------------------------------------------------
+// phi_e.0 per edge in fp32: [h_s | h_r | |r|^2] W1 + b1 (egnn.py:76-79), natural-domain SiLU and its tangent.  A =
+// the fp32 kernel rows read in place from the node-GEMM copy Wp = [W_send | W_recv] ([H][2M]) and w_d, B = feature
+// k0 + kk of the lane's edge from the hb rows (tangent rows RP + n); primal and tangent share every A value.
+template <int NF>
+__device__ __forceinline__ void edge_layer1_dual_f32(const Net& net, const BlockW& bw, const Lds& s, int rr, int rs,
+                                                     float len2, float dlen2, f32x16 (&X)[NF], f32x16 (&XT)[NF],
+                                                     int lane) {
+  const int kk = lane >> 5, li = lane & 31, H = net.H, RP = net.RP, M = NF * 32;
+#pragma unroll
+  for (int jb = 0; jb < NF; ++jb) {
+    X[jb] = f32x16{};
+    XT[jb] = f32x16{};
+  }
+  const gfloat_p wp = gptr(launder_uniform(bw.Wp));
+  // k-steps of 2 over h_s (columns 0 .. M-1 of Wp) and h_r (columns M .. 2M-1): lane half kk holds feature k0 + kk
+  for (int part = 0; part < 2; ++part) {
+    const float* hrow = s.hb + (part ? rr : rs) * s.ld_hb + kk;
+    const float* hrowT = s.hb + (RP + (part ? rr : rs)) * s.ld_hb + kk;
+    const gfloat_p wcol = wp + kk * 2 * M + part * M + li;
+    for (int k0 = 0; k0 < H; k0 += 2) {
+      const float b = hrow[k0], bt = hrowT[k0];
+      static_for<NF>([&](auto Jc) {
+        constexpr int jb = decltype(Jc)::value;
+        const float a = wcol[k0 * 2 * M + jb * 32];
+        X[jb] = mfma32(a, b, X[jb]);
+        XT[jb] = mfma32(a, bt, XT[jb]);
+      });
+    }
+  }
+  {  // the |r|^2 row (k = 2H on lane half 0; half 1 holds the zero padding k = 2H + 1)
+    const float b = kk ? 0.f : len2, bt = kk ? 0.f : dlen2;
+    const gfloat_p wd = gptr(launder_uniform(bw.wd)) + li;
+    static_for<NF>([&](auto Jc) {
+      constexpr int jb = decltype(Jc)::value;
+      const float a = kk ? 0.f : wd[jb * 32];
+      X[jb] = mfma32(a, b, X[jb]);
+      XT[jb] = mfma32(a, bt, XT[jb]);
+    });
+  }
+#pragma unroll
+  for (int jb = 0; jb < NF; ++jb)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const f32x4 b4 = gptr4(bw.bp + M + jb * 32 + 8 * q + 4 * kk)[0];   // bias [0 | b1]
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int r = 4 * q + e;
+        float y, yT;
+        silu_dual<1>(X[jb][r] + b4[e], XT[jb][r], y, yT);
+        X[jb][r] = y;
+        XT[jb][r] = yT;
+      }
+    }
+}
+
+// one fp32 pass of a chain layer: acc[jb] = sum over fb of W[l][jb][fb] X[fb] (16 k-steps of 2 per 32-row input
+// block), the fp32 fragments of chain_segment ([layer][jb][fb][q][lane][4]) streamed PF groups ahead
+template <int NF>
+__device__ __forceinline__ void dual_pass_f32(const f32x16 (&X)[NF], f32x16 (&acc)[NF], gf32x4_p wl) {
+#ifndef ECNF_W32_PF
+#define ECNF_W32_PF 2
+#endif
+  constexpr int G = NF * NF, PF = ECNF_W32_PF;
+  f32x4 wbuf[PF + 1][4];
+  static_for<PF>([&](auto Gc) {
+    constexpr int gg = decltype(Gc)::value;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) wbuf[gg][q] = wl[(gg * 4 + q) * 64];
+  });
+  static_for<G>([&](auto Gc) {
+    constexpr int gg = decltype(Gc)::value;
+    constexpr int jb = gg / NF, fb = gg % NF;   // group (jb, fb) sits at wl[((jb * NF + fb) * 4 + q) * 64]
+    if constexpr (gg + PF < G) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) wbuf[(gg + PF) % (PF + 1)][q] = wl[((gg + PF) * 4 + q) * 64];
+    }
+    if constexpr (fb == 0) acc[jb] = f32x16{};
+    static_for<16>([&](auto Ic) {
+      constexpr int i = decltype(Ic)::value;
+      acc[jb] = mfma32(wbuf[gg % (PF + 1)][i >> 2][i & 3], X[fb][i], acc[jb]);
+    });
+    __builtin_amdgcn_sched_barrier(0);
+  });
+}
+
+// NL chain layers X <- silu(X W + b) with forward-mode tangents, the primal and the tangent in sequential passes
+// over the same fp32 fragments (as chain_dual_seq): at most X, XT and one accumulator set (3 x 128 registers) live.
+// bias: the natural-domain chain biases staged in LDS ([NL][M]).
+template <int NF, int NL>
+__device__ __forceinline__ void chain_dual_seq_f32(f32x16 (&X)[NF], f32x16 (&XT)[NF], const float* __restrict__ Wpk,
+                                                   const float* __restrict__ bias, int lane) {
+  constexpr int M = NF * 32;
+  const int kk = lane >> 5;
+  for (int l = 0; l < NL; ++l) {
+    // the layer's fragments through launder_uniform once per pass: the tangent pass must load them again (plain
+    // loads of one address would be merged with the primal pass's, keeping 1024 weight values live across it)
+    const size_t loff = (size_t)l * NF * NF * 4 * 64 + lane;
+    f32x16 acc[NF];
+    dual_pass_f32<NF>(X, acc, gptr4(launder_uniform(Wpk)) + loff);    // acc = W X
+    __builtin_amdgcn_sched_barrier(0);
+    dual_pass_f32<NF>(XT, X, gptr4(launder_uniform(Wpk)) + loff);     // X (dead after the primal pass) <- W X_T
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int fb = 0; fb < NF; ++fb)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f32x4 b4 = *reinterpret_cast<const f32x4*>(bias + l * M + fb * 32 + 8 * q + 4 * kk);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int r = 4 * q + e;
+          float y, yT;
+          silu_dual<1>(acc[fb][r] + b4[e], X[fb][r], y, yT);
+          X[fb][r] = y;
+          XT[fb][r] = yT;
+        }
+      }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
 // one 32-edge tile through phi_e / gate / phi_x  (egnn.py:72-95)
 // a >= 0 (split tangent kernels only, exact trace, egnn_eval sparse_a): `tile` is a molecule and the tile is dual
 // tile `part` of 2(N - 1) edges of that molecule, in receiver-major order, storing tangent outputs only.
@@ -1340,6 +1497,21 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
     STAMP_LANE0(s, kStEdgeTail, t_sub);
     return;
   }
+  if constexpr (Geo<NF, NT, P>::kWideT32) {
+    // the same in strict fp32 (natural-domain activations and biases, the fp32 chain fragments)
+    f32x16 X[NF], XT[NF];
+    edge_layer1_dual_f32<NF>(net, bw, s, rr, rs, len2, dlen2, X, XT, lane);
+    STAMP_LANE0(s, kStEdgeLayer1, t_sub);
+    chain_dual_seq_f32<NF, L - 1>(X, XT, launder_uniform(bw.We), s.vecs, lane);
+    STAMP_LANE0(s, kStEdgeChainE, t_sub);
+    edge_tail<NF, NT, L, D>(net, bw, s, X, XT, valid, rr, agg_dst, r, dr, length, dlength, lane, agg,
+                            [&](f32x16 (&Y)[NF], f32x16 (&YT)[NF]) {
+                              const float* Wx = launder_uniform(bw.We + (size_t)(L - 1) * NF * NF * 1024);
+                              chain_dual_seq_f32<NF, L>(Y, YT, Wx, s.vecs + (L - 1) * NF * 32, lane);
+                            });
+    STAMP_LANE0(s, kStEdgeTail, t_sub);
+    return;
+  }
   // phi_e layer 1 from the per-node halves: pre = P_s[s] + P_r[r] + |r|^2 w_d  (egnn.py:76,79)
   f32x16 X[NF], XT[NF];
   const float* Ps = s.P + rs * s.ld_P;
@@ -1489,7 +1661,7 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
     __syncthreads();
     STAMP(s, kStNodeDense);
     // per-node halves of phi_e layer 1 (the M = 256 tangent kernels compute layer 1 per edge)
-    if constexpr (!Geo<NF, NT, P>::kWideT) {
+    if constexpr (!Geo<NF, NT, P>::kNoP) {
       constexpr bool kPu = kSplitG || Geo<NF, NT, P>::kL2T;   // log2-domain P
       node_gemm<NT, kNW, kSplitN>(s.hb, s.ld_hb, H, nullptr, 0, 0, bw.Wp, bw.Wp_s, bw.pinv, 2 * M,
                                   kPu ? bw.bp_u : bw.bp, 2 * M, false, nullptr, 0, s.P, s.ld_P, RP, nvalid, wave, lane);
@@ -1653,6 +1825,26 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
       }
       node_gemm<NT, kNW, true>(s.macc, s.ld_m, M, nullptr, 0, 0, bw.Wh[L], bw.Wh_s[L], bw.hinv[L], H, bw.bh[L], H, false,
                                s.hb, s.ld_hb, s.hin, s.ld_hin, RP, nvalid, wave, lane);
+      __syncthreads();
+      for (int idx = tid; idx < R * M; idx += kNT) {
+        const int row = idx / M, c = idx - row * M;
+        s.macc[row * s.ld_m + c] = 0.f;
+      }
+      __syncthreads();
+      STAMP(s, kStPhiH);
+      continue;
+    }
+    if constexpr (Geo<NF, NT, P>::kWideT32) {   // the same in fp32 (macc already carries the 1 / sqrt(N - 1))
+      node_gemm_inplace_f32<NT, kNW>(s.macc, s.ld_m, M, s.hb, s.ld_hb, H, bw.Wh[0], M, bw.bh[0], M, true, s.macc,
+                                     s.ld_m, RP, nvalid, wave, lane);
+      __syncthreads();
+      for (int l = 1; l < L; ++l) {
+        node_gemm_inplace_f32<NT, kNW>(s.macc, s.ld_m, M, nullptr, 0, 0, bw.Wh[l], M, bw.bh[l], M, true, s.macc,
+                                       s.ld_m, RP, nvalid, wave, lane);
+        __syncthreads();
+      }
+      node_gemm<NT, kNW, false>(s.macc, s.ld_m, M, nullptr, 0, 0, bw.Wh[L], nullptr, 1.0f, H, bw.bh[L], H, false,
+                                s.hb, s.ld_hb, s.hin, s.ld_hin, RP, nvalid, wave, lane);
       __syncthreads();
       for (int idx = tid; idx < R * M; idx += kNT) {
         const int row = idx / M, c = idx - row * M;

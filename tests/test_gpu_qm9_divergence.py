@@ -1,6 +1,8 @@
 """GPU parity of the M = 256 tangent kernels (QM9, Geo::kWideT: per-edge phi_e.0, sequential primal / tangent split
-chains, in-place phi_h) against the CPU oracle: the JVP, the Hutchinson log-density of get_log_prob /
-sample_and_log_prob_cnf on the qm9.yaml network (N = 29), and the exact trace on a small-N M = 256 network.
+chains, in-place phi_h; Geo::kWideT32: the same structure in strict fp32) against the CPU oracle: the JVP, the
+Hutchinson log-density of get_log_prob / sample_and_log_prob_cnf on the qm9.yaml network (N = 29), and the exact trace
+on a small-N M = 256 network, at both GEMM precisions; a checkpoint with an edge weight >= 2^15 runs its divergence on
+the strict-fp32 kernels.
 
 Reference: setup_training.py:190-203 (get_log_prob on the test set for every config), sample_and_log_prob.py:41-149,
 examples/config/qm9.yaml:5-13.  Tolerances as tests/test_gpu_parity.py: JVP max |err| <= 2e-5 * max(1, |ref|);
@@ -19,7 +21,7 @@ if not torch.cuda.is_available():  # collected on CPU-only hosts, skipped there
 
 from ecnf_amd import CONFIGS, CNFConfig  # noqa: E402
 from ecnf_amd import _lib  # noqa: E402
-from ecnf_amd.engine import SolveOptions  # noqa: E402
+from ecnf_amd.engine import EcnfHandle, SolveOptions  # noqa: E402
 
 from test_gpu_parity import g, rel_err, setup  # noqa: E402
 
@@ -28,17 +30,31 @@ WIDE_TINY = CNFConfig(n_nodes=5, dim=3, n_features=2, hidden=32, mlp_width=256, 
                       base_scale=1.0)
 
 
-def test_qm9_tangent_kernel_exists():
+_FP32 = {}
+
+
+def setup_prec(cfg, B, precision):
+    """setup() of test_gpu_parity, with a strict-fp32 handle of the same weights for precision == "fp32"."""
+    oc, params, h, z, x0, feat = setup(cfg, B)
+    if precision == "fp32":
+        if cfg not in _FP32:
+            _FP32[cfg] = EcnfHandle(cfg, params, 0, precision="fp32")
+        h = _FP32[cfg]
+    return oc, params, h, z, x0, feat
+
+
+@pytest.mark.parametrize("precision", ["split_f16", "fp32"])
+def test_qm9_tangent_kernel_exists(precision):
     cfg = CONFIGS["qm9"]
-    _, _, h, _, _, _ = setup(cfg, B=1)
+    _, _, h, _, _, _ = setup_prec(cfg, 1, precision)
     assert h.molecules_per_workgroup(with_tangent=True) == 1
-    assert h.chain_arithmetic(with_tangent=True) == "split_f16"
+    assert h.chain_arithmetic(with_tangent=True) == ("split_f16" if precision == "split_f16" else "fp32_mfma")
 
 
-@pytest.mark.parametrize("name", ["qm9"])
-def test_jvp_wide(name):
-    cfg = CONFIGS[name]
-    oc, params, h, z, x0, feat = setup(cfg, B=3)
+@pytest.mark.parametrize("precision", ["split_f16", "fp32"])
+def test_jvp_wide(precision):
+    cfg = CONFIGS["qm9"]
+    oc, params, h, z, x0, feat = setup_prec(cfg, 3, precision)
     t = np.array([0.1, 0.5, 0.9], np.float32)
     u = np.random.default_rng(3).standard_normal((3, 2, cfg.event_dim)).astype(np.float32)
     v, ju = h.jvp(g(x0), g(t), g(feat, torch.int32), g(u))
@@ -47,10 +63,11 @@ def test_jvp_wide(name):
     assert rel_err(ju, jr) <= 2e-5, rel_err(ju, jr)
 
 
-def test_qm9_log_prob_hutchinson_fixed():
+@pytest.mark.parametrize("precision", ["split_f16", "fp32"])
+def test_qm9_log_prob_hutchinson_fixed(precision):
     """get_log_prob(approx=True, fixed steps) on qm9.yaml: 1 -> 0, 8 Euler steps."""
     cfg = CONFIGS["qm9"]
-    oc, params, h, z, x0, feat = setup(cfg, B=2)
+    oc, params, h, z, x0, feat = setup_prec(cfg, 2, precision)
     eps = np.random.default_rng(77).standard_normal(x0.shape).astype(np.float32)
     x, dl, nfe, st = h.integrate(g(x0), g(feat, torch.int32), 1.0, 0.0, SolveOptions("euler", 0.125),
                                  divergence=_lib.DIV_HUTCHINSON, eps=g(eps))
@@ -78,10 +95,11 @@ def test_qm9_sample_and_log_prob_hutchinson():
     fp32_class("qm9 s+lp log_q", lq, lq_ref, lq_32)
 
 
-def test_wide_log_prob_exact_fixed():
+@pytest.mark.parametrize("precision", ["split_f16", "fp32"])
+def test_wide_log_prob_exact_fixed(precision):
     """get_log_prob(approx=False): the full N*D trace through the M = 256 tangent kernels (small N)."""
     cfg = WIDE_TINY
-    oc, params, h, z, x0, feat = setup(cfg, B=3)
+    oc, params, h, z, x0, feat = setup_prec(cfg, 3, precision)
     x, dl, nfe, _ = h.integrate(g(x0), g(feat, torch.int32), 1.0, 0.0, SolveOptions("euler", 0.125),
                                 divergence=_lib.DIV_EXACT)
     r64 = O.get_log_prob(params, oc, x0, feat, approx=False, solver="euler", dt0=0.125, dtype=np.float64)
@@ -90,3 +108,31 @@ def test_wide_log_prob_exact_fixed():
     fp32_class("wide exact dl", dl, r64[2], r32[2])
     lp = (h.base_log_prob(x) + dl).cpu().numpy()
     fp32_class("wide exact log_p", lp, r64[0], r32[0])
+
+
+def test_wide_huge_weight_divergence_runs_strict_fp32():
+    """An edge-MLP weight >= 2^15 on the M = 256 network: ecnf_create makes the handle strict fp32 and its divergence
+    solves run on the fp32 M = 256 tangent kernels (round 2 refused them with ECNF_E_UNSUPPORTED)."""
+    cfg = WIDE_TINY
+    oc, _, _, z, x0, feat = setup(cfg, B=3)
+    p = dict(O.init_params(oc, 0))
+    w = p["EGNN_0/1/phi_x_torso/Dense_1/kernel"].copy()
+    w[3, 5] = 40000.0
+    p["EGNN_0/1/phi_x_torso/Dense_1/kernel"] = w
+    h = EcnfHandle(cfg, p, 0)
+    assert h.precision == "fp32" and h.chain_arithmetic(with_tangent=True) == "fp32_mfma"
+    t = np.array([0.2, 0.5, 0.8], np.float32)
+    u = np.random.default_rng(4).standard_normal((3, 2, cfg.event_dim)).astype(np.float32)
+    v, ju = h.jvp(g(x0), g(t), g(feat, torch.int32), g(u))
+    vr, jr = O.egnn_vector_field(p, oc, x0, t, feat, tangents=u, dtype=np.float64)
+    vr32, jr32 = O.egnn_vector_field(p, oc, x0, t, feat, tangents=u, dtype=np.float32)
+    fp32_class("wide huge-weight v", v, vr, vr32)
+    fp32_class("wide huge-weight jvp", ju, jr, jr32)
+    eps = np.random.default_rng(5).standard_normal(x0.shape).astype(np.float32)
+    x, dl, nfe, st = h.integrate(g(x0), g(feat, torch.int32), 1.0, 0.0, SolveOptions("euler", 0.5),
+                                 divergence=_lib.DIV_HUTCHINSON, eps=g(eps))
+    r64 = O.get_log_prob(p, oc, x0, feat, eps=eps, approx=True, solver="euler", dt0=0.5, dtype=np.float64)
+    r32 = O.get_log_prob(p, oc, x0, feat, eps=eps, approx=True, solver="euler", dt0=0.5, dtype=np.float32)
+    assert int(st.abs().sum()) == 0
+    fp32_class("wide huge-weight x", x, r64[4], r32[4])
+    fp32_class("wide huge-weight dl", dl, r64[2], r32[2])
