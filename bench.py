@@ -240,8 +240,7 @@ def main():
     ap.add_argument("--config", default="lj13")
     ap.add_argument("--nfe", type=int, default=100)
     ap.add_argument("--logprob", type=int, default=-1,
-                    help="eval leg (sample + Hutchinson log-prob + target + ESS) passes: default 1 over several ranks, "
-                         "0 at one rank")
+                    help="eval leg (sample + Hutchinson log-prob + target + ESS) passes (default 1)")
     ap.add_argument("--fp32-steps", type=int, default=2, help="launches of the strict-fp32 kernels timed (0 = skip)")
     ap.add_argument("--train-steps", type=int, default=10, help="timed training steps at N = 1 (0 = skip)")
     ap.add_argument("--train-batch", type=int, default=64, help="training batch (lj13.yaml: 64)")
@@ -286,7 +285,7 @@ def main():
     G = args.batch or (GLOBAL_BATCH_MULTI if world > 1 else 1024)
     lo, hi = D.shard_bounds(G, rank, world)
     B = hi - lo
-    n_logprob = args.logprob if args.logprob >= 0 else (1 if world > 1 else 0)
+    n_logprob = args.logprob if args.logprob >= 0 else 1
 
     h = EcnfHandle(cfg, init_params(cfg, 0), local)
     z = D.global_normal(G, cfg.event_dim, args.seed, lo, hi, dev)     # rows [lo, hi) of one global draw
@@ -370,8 +369,11 @@ def main():
             barrier()
             torch.cuda.synchronize(dev)
             t1 = time.perf_counter()
+            ek0, ek1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            ek0.record(stream)
             x1, dl, _, st = h.integrate(x0, feat, 0.0, 1.0, opts, divergence=_lib.DIV_HUTCHINSON, eps=z,
                                         check_status=False)
+            ek1.record(stream)
             log_q = h.base_log_prob(x0) - dl          # sample_and_log_prob.py:147 (eps = z: the ref's quirk)
             log_p = T.lj_log_prob(x1, cfg.n_nodes, cfg.dim) if args.config == "lj13" else \
                 T.dw_log_prob(x1, cfg.n_nodes, cfg.dim)
@@ -385,7 +387,11 @@ def main():
             t_lp = max_over_ranks(time.perf_counter() - t1)
         logprob = {"workload": f"{args.config} sample_and_log_prob_cnf (Hutchinson, Euler NFE={args.nfe}) + target "
                                f"log-density + ESS over {'RCCL' if args.dist_backend == 'nccl' else args.dist_backend}",
-                   "molecules_per_s": G / t_lp, "ms": t_lp * 1e3, "rev_ess": float(rev),
+                   "molecules_per_s": G / t_lp, "ms": t_lp * 1e3,
+                   # the divergence kernel alone (HIP events on its stream): primal + one tangent per evaluation
+                   "kernel_ms": ek0.elapsed_time(ek1),
+                   "achieved_tflops": 2 * F * nfe_seen * B / (ek0.elapsed_time(ek1) * 1e-3) / 1e12 if B else 0.0,
+                   "tangent_kernels": h.chain_arithmetic(with_tangent=True), "rev_ess": float(rev),
                    "mean_log_q": float(mean_lq), "status_ok": bool(int((st != 0).sum()) == 0)}
         if args.dump:
             os.makedirs(args.dump, exist_ok=True)
