@@ -652,7 +652,10 @@ __device__ __forceinline__ void node_gemm(const float* X1, int ldx1, int K1, con
                                           int ldr, float* Y, int ldy, int RP, int nvalid, int wave, int lane) {
   const int njb = NOUT >> 5, nct = RP >> 5;
   if constexpr (SPLIT) {
-    if ((njb % 2) == 0 && (njb / 2) * nct >= NW) {   // two output blocks per task share the B split
+#ifndef ECNF_NODE_PAIR_DIV
+#define ECNF_NODE_PAIR_DIV 1
+#endif
+    if ((njb % 2) == 0 && (njb / 2) * nct >= NW / ECNF_NODE_PAIR_DIV) {   // two output blocks per task share the B split
       const int npair = njb / 2;
       for (int task = wave; task < npair * nct; task += NW)
         node_task_split<2, NT>(X1, ldx1, K1, X2, ldx2, K2, Ws, winv, bias, act, resid, ldr, Y, ldy, RP, nvalid,
