@@ -46,3 +46,18 @@ def test_split_kernels_do_not_spill():
         if scratch > limit:
             bad.append(f"{kind}<{nf},{nt},{l},{d},{p}> scratch {scratch} B/lane (limit {limit})")
     assert not bad, "\n".join(bad)
+
+
+def test_strict_fp32_tangent_kernels_exist_for_every_shape():
+    """Every compiled shape has tangent kernels at both precisions, M = 256 included (Geo::kWideT32, round 3: the
+    strict-fp32 route for QM9 divergence solves and >= 2^15 weights).  Their sequential fp32 chain passes keep a
+    bounded spill (364 B/lane at build time; the weight loads of the two passes must not be merged, which once
+    spilled 4.3 KB/lane)."""
+    ks = _kernels()
+    shapes = {(nf, l, d) for kind, nf, nt, l, d, p, s in ks if kind == "integrate_kernel"}
+    have = {(nf, nt, l, d, p) for kind, nf, nt, l, d, p, s in ks if kind == "integrate_kernel"}
+    missing = [(nf, nt, l, d, p) for nf, l, d in shapes for nt in (0, 1) for p in (0, 1)
+               if (nf, nt, l, d, p) not in have]
+    assert not missing, missing
+    wide32 = [(l, d, s) for kind, nf, nt, l, d, p, s in ks if nf == 8 and nt == 1 and p == 1]
+    assert wide32 and all(s <= 512 for _, _, s in wide32), wide32
