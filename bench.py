@@ -18,8 +18,10 @@ CHILD process, before this process touches the GPU) and exits with its status; u
 Extra fields: "roofline" (dominant kernel = integrate_kernel, MFMA bound: algorithmic fp32 FLOPs per launch /
 average launch time from HIP events on the launch stream, against the ceiling of the kernel's instruction mix —
 GEMM FLOPs at the split-fp16 rate, vector FLOPs at the fp32 rate; see roofline_peak), "matmul" (which arithmetic the
-GEMMs run, and the strict-fp32 kernels' time on the same workload), "logprob" (the eval leg), "train" (the
-flow-matching training step at lj13.yaml's batch 64) and "cpu_baseline" (a
+GEMMs run, and the strict-fp32 kernels' time on the same workload), "logprob" (the eval leg, at every N: the
+Hutchinson divergence kernel's time and TFLOP/s), "train" (the flow-matching training step at lj13.yaml's batch 64),
+"ref_sampling_latency" (the reference's own timing script: one QM9 molecule per adaptive sample_cnf call) and
+"cpu_baseline" (a
 torch-CPU fp32 batched restatement of the same Euler solve on a bounded sample, rank 0 at N = 1 only).
 """
 from __future__ import annotations
@@ -244,6 +246,8 @@ def main():
     ap.add_argument("--fp32-steps", type=int, default=2, help="launches of the strict-fp32 kernels timed (0 = skip)")
     ap.add_argument("--train-steps", type=int, default=10, help="timed training steps at N = 1 (0 = skip)")
     ap.add_argument("--train-batch", type=int, default=64, help="training batch (lj13.yaml: 64)")
+    ap.add_argument("--ref-latency-samples", type=int, default=10,
+                    help="calls of the reference's single-molecule QM9 sampling-time script (first = warm-up; 0 = skip)")
     ap.add_argument("--cpu-molecules", type=int, default=256, help="bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--cpu-molecules-1t", type=int, default=48, help="bounded 1-thread CPU-baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "0") or 0))
@@ -399,6 +403,33 @@ def main():
                      x1_lp=x1.cpu().numpy(), log_q=log_q.cpu().numpy(), log_w=log_w.cpu().numpy(),
                      rev_ess=float(rev), mean_log_q=float(mean_lq), world=world)
 
+    # the reference's own timing script (examples/load_checkpoint_measure_sampling_time.py:104-126): qm9.yaml
+    # network, ONE molecule per sample_cnf call with the default adaptive solve (Dopri5 + PIDController rtol = atol =
+    # 1e-5), 10 calls of which the first is the warm-up; wall time per call incl. the host round trip.  Random-init
+    # weights (the script loads a trained wandb checkpoint, unavailable offline), so the step count differs.
+    ref_latency = None
+    if world == 1 and args.ref_latency_samples > 1:
+        qcfg = CONFIGS["qm9"]
+        hq = EcnfHandle(qcfg, init_params(qcfg, 0), local)
+        gq = torch.Generator(device=dev)
+        gq.manual_seed(0)
+        fq = torch.zeros((1, qcfg.n_nodes), device=dev, dtype=torch.int32)
+        times, nfes = [], []
+        for i in range(args.ref_latency_samples):
+            zq = torch.randn((1, qcfg.event_dim), generator=gq, device=dev)
+            torch.cuda.synchronize(dev)
+            t1 = time.perf_counter()
+            xq, _, nq, sq = hq.integrate(hq.base_sample(zq), fq, 0.0, 1.0, SolveOptions("dopri5", None))
+            xq.cpu()                                   # the sample reaches the host, as jax's result does
+            if i:
+                times.append(time.perf_counter() - t1)
+                nfes.append(int(nq.max()))
+        ref_latency = {"workload": "qm9 sample_cnf, 1 molecule per call, Dopri5 + PID rtol=atol=1e-5 "
+                                   "(load_checkpoint_measure_sampling_time.py:104-126), random-init weights",
+                       "ms_median": 1e3 * float(np.median(times)), "ms_min": 1e3 * float(np.min(times)),
+                       "nfe_median": float(np.median(nfes)), "calls": len(times)}
+        del hq
+
     # training leg (SURVEY 8f rank 3, lj13.yaml training: Adam, batch 64): one flow_matching_update_fn step =
     # loss + reverse-mode gradient + Adam, on the same device (N = 1 only)
     train = None
@@ -484,6 +515,7 @@ def main():
                                        else "fp32 MFMA peak"},
             "logprob": logprob,
             "train": train,
+            "ref_sampling_latency": ref_latency,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
