@@ -780,7 +780,7 @@ int ecnf_create(const ecnf_cfg* cfg, const float* params, size_t n_floats, int d
   bool split_ok = true;   // every edge-chain weight fits the unscaled fp16 split (|w| < 2^15)
   struct Off {
     size_t Wn, bn, Wp, bp, wd, We, Ws, be, wx, wg, Wh[kMaxPhiH], bh[kMaxPhiH], Wn_s, Wp_s, Wh_s[kMaxPhiH];
-    size_t bp_u, wd_u, be_u, wg_u, wx_u, Wh_sn0, W1_s, Ws3;
+    size_t bp_u, wd_u, be_u, wg_u, wx_u, Wh_sn0, W1_s, Ws3, bnp_u;
     float bx, bg, hinv_n0, w1inv;
     float cinv[2 * 4 - 1], ninv, pinv, hinv[kMaxPhiH];
   };
@@ -814,8 +814,30 @@ int ecnf_create(const ecnf_cfg* cfg, const float* params, size_t n_floats, int d
       for (auto& x : r) x *= f;
       return r;
     };
-    const std::vector<float> wp_u = scaled(wp.data(), wp.size(), kNegLog2e);
-    o.Wp_s = put_split_node(wp_u.data(), H, 2 * M, &o.pinv);
+    if (ECNF_FUSED_P) {
+      // fused node Dense + phi_e.0 halves (Geo::kFusedP): -log2(e) x W_n W_p over the [h | temb] rows and the bias
+      // -log2(e) x (b_n W_p + [0 | b1]), products in double, rounded once
+      std::vector<double> acc((size_t)(H + T) * 2 * M, 0.0), bacc(2 * M, 0.0);
+      for (int r = 0; r < H + T; ++r)
+        for (int q = 0; q < H; ++q) {
+          const double a = b.nk[(size_t)r * H + q];
+          for (int j = 0; j < 2 * M; ++j) acc[(size_t)r * 2 * M + j] += a * wp[(size_t)q * 2 * M + j];
+        }
+      for (int j = 0; j < 2 * M; ++j) {
+        double v = bp[j];
+        for (int q = 0; q < H; ++q) v += (double)b.nb[q] * wp[(size_t)q * 2 * M + j];
+        bacc[j] = v;
+      }
+      std::vector<float> wnp_u(acc.size()), bnp_u(2 * M);
+      for (size_t i = 0; i < acc.size(); ++i) wnp_u[i] = (float)(acc[i] * (double)kNegLog2e);
+      for (int j = 0; j < 2 * M; ++j) bnp_u[j] = (float)(bacc[j] * (double)kNegLog2e);
+      o.Wp_s = put_split_node(wnp_u.data(), H + T, 2 * M, &o.pinv);
+      o.bnp_u = pk.put(bnp_u.data(), bnp_u.size());
+    } else {
+      const std::vector<float> wp_u = scaled(wp.data(), wp.size(), kNegLog2e);
+      o.Wp_s = put_split_node(wp_u.data(), H, 2 * M, &o.pinv);
+      o.bnp_u = 0;
+    }
     // the M = 256 tangent kernels' per-edge phi_e.0: [h_s | h_r | |r|^2] rows 0 .. 2H of the kernel, x -log2(e)
     o.W1_s = put_split_node(scaled(b.ek[0], (size_t)(2 * H + 1) * M, kNegLog2e).data(), 2 * H + 1, M, &o.w1inv);
     o.bp_u = pk.put(scaled(bp.data(), bp.size(), kNegLog2e).data(), bp.size());
@@ -955,6 +977,7 @@ int ecnf_create(const ecnf_cfg* cfg, const float* params, size_t n_floats, int d
       w.Wh_sn0 = reinterpret_cast<const unsigned*>(dbuf + o.Wh_sn0);
       w.hinv_n0 = o.hinv_n0;
       w.W1_s = reinterpret_cast<const unsigned*>(dbuf + o.W1_s);
+      w.bnp_u = dbuf + o.bnp_u;
       w.w1inv = o.w1inv;
       w.Ws3 = reinterpret_cast<const unsigned*>(dbuf + o.Ws3);
     }

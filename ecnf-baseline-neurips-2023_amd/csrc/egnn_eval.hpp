@@ -82,6 +82,12 @@ struct Geo {
   static constexpr bool kWideT32 = P == 1 && NT == 1 && NF == 8;
   static constexpr bool kNoP = kWideT || kWideT32;   // no per-node phi_e.0 halves (P rows) in LDS
   static constexpr bool kSplitN = kSplit || (kSplitTanNode && kSplitT) || kWideT;
+#ifndef ECNF_FUSED_P
+#define ECNF_FUSED_P 1
+#endif
+  // the split kernels with per-node phi_e.0 halves compute them from hin with the host-fused W_n W_p in the same node
+  // phase as the node Dense (one barrier and one GEMM latency less per block; egnn_eval)
+  static constexpr bool kFusedP = ECNF_FUSED_P && kSplitN && !kNoP;
   // M <= 128 split tangent kernels: P (primal and tangent rows) in the log2 domain (the primal kernels' -log2(e)
   // fragments), phi_e.0's SiLU and its tangent evaluated there and split straight into the chain's input buffers
   static constexpr bool kL2T = kSplitT && kSplitN;
@@ -156,6 +162,9 @@ struct BlockW {
   // M = 256 tangent kernels: phi_e.0 kernel [(2H+1)][M] x -log2(e) as split node fragments (edge_layer1_dual)
   const unsigned* W1_s;
   float w1inv;
+  // fused-P split kernels (kFusedP): Wp_s / pinv hold -log2(e) x W_n W_p over the [h | temb] rows (K = H + T), so the
+  // phi_e.0 halves come straight from hin in the node-Dense phase; bnp_u = -log2(e) x (b_n W_p + [0 | b1])
+  const float* bnp_u;
   // the divergence kernels' chain: every chain layer scaled by a power of two and split into THREE fp16 pieces that
   // hold the fp32 weight exactly (chain_split WP = 3); 1 / the scales are cinv (the 2-piece chain Ws is unscaled and
   // ignores them with ECNF_CHAIN_BIAS_INIT, and uses the same scales without it)
@@ -1659,6 +1668,16 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
       }
     }
     // h <- Dense([h | temb])  (egnn.py:166-167)
+    if constexpr (Geo<NF, NT, P>::kFusedP) {
+      // ... and, in the same phase, the per-node phi_e.0 halves P = [h | temb] (W_n W_p) + (b_n W_p + [0 | b1]) in
+      // the log2 domain (host-fused weights), with the Dense tasks dealt from the other end of the waves
+      node_gemm<NT, kNW, true>(s.hin, s.ld_hin, H + T, nullptr, 0, 0, bw.Wn, bw.Wn_s, bw.ninv, H, bw.bn, H, false,
+                               nullptr, 0, s.hb, s.ld_hb, RP, nvalid, kNW - 1 - wave, lane);
+      node_gemm<NT, kNW, true>(s.hin, s.ld_hin, H + T, nullptr, 0, 0, bw.Wp, bw.Wp_s, bw.pinv, 2 * M, bw.bnp_u, 2 * M,
+                               false, nullptr, 0, s.P, s.ld_P, RP, nvalid, wave, lane);
+      __syncthreads();
+      STAMP(s, kStNodeDense);
+    } else {
     node_gemm<NT, kNW, kSplitN>(s.hin, s.ld_hin, H + T, nullptr, 0, 0, bw.Wn, bw.Wn_s, bw.ninv, H, bw.bn, H, false, nullptr, 0, s.hb, s.ld_hb, RP,
                   nvalid, wave, lane);
     __syncthreads();
@@ -1670,6 +1689,7 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
                                   kPu ? bw.bp_u : bw.bp, 2 * M, false, nullptr, 0, s.P, s.ld_P, RP, nvalid, wave, lane);
       __syncthreads();
     }
+    }   // !kFusedP
     STAMP(s, kStPGemm);
     // edges
     // tile t runs on wave t mod NW, i.e. SIMD t mod 4: every SIMD gets ceil/floor(ntiles / 4) tiles
