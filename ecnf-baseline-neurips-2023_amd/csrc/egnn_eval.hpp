@@ -83,10 +83,12 @@ struct Geo {
   static constexpr bool kNoP = kWideT || kWideT32;   // no per-node phi_e.0 halves (P rows) in LDS
   static constexpr bool kSplitN = kSplit || (kSplitTanNode && kSplitT) || kWideT;
 #ifndef ECNF_FUSED_P
-#define ECNF_FUSED_P 1
+#define ECNF_FUSED_P 0
 #endif
-  // the split kernels with per-node phi_e.0 halves compute them from hin with the host-fused W_n W_p in the same node
-  // phase as the node Dense (one barrier and one GEMM latency less per block; egnn_eval)
+  // experiment (-DECNF_FUSED_P=1, measured, not adopted): the split kernels with per-node phi_e.0 halves compute them
+  // from hin with the host-fused W_n W_p in the same node phase as the node Dense (one barrier and one GEMM latency
+  // less per block, but K = H + T instead of H for the P GEMM): LJ13 26.02 vs 25.92 ms, LJ13 Hutchinson 63.84 vs
+  // 63.89, ALDP PID sample 3.25 vs 3.21, ALDP Hutchinson 29.84 vs 30.51 ms (profiles/round3/ab/tvf_*.log)
   static constexpr bool kFusedP = ECNF_FUSED_P && kSplitN && !kNoP;
   // M <= 128 split tangent kernels: P (primal and tangent rows) in the log2 domain (the primal kernels' -log2(e)
   // fragments), phi_e.0's SiLU and its tangent evaluated there and split straight into the chain's input buffers
