@@ -174,7 +174,8 @@ class EcnfHandle:
         return v.value
 
     def _fp32_available(self, with_tangent: bool) -> bool:
-        """Whether the strict-fp32 kernels exist for this shape (the M = 256 tangent kernels are split-fp16 only)."""
+        """Whether the strict-fp32 kernels exist for this shape and fit the LDS (every compiled shape has them, the
+        M = 256 tangent kernels included since round 3; a tangent kernel can still miss the LDS at large N)."""
         prev = self.precision
         self._set_precision("fp32")
         try:
