@@ -136,3 +136,32 @@ def test_wide_huge_weight_divergence_runs_strict_fp32():
     assert int(st.abs().sum()) == 0
     fp32_class("wide huge-weight x", x, r64[4], r32[4])
     fp32_class("wide huge-weight dl", dl, r64[2], r32[2])
+
+
+def test_wide_nonfinite_divergence_reruns_on_strict_fp32():
+    """A molecule whose activations leave the fp16 range in the split M = 256 tangent kernels reports
+    ECNF_E_NONFINITE; with the host fallback it is solved again on the strict-fp32 M = 256 tangent kernels (round 2
+    had none: the molecule stayed flagged) and its log-density is fp32-class; the other molecules are unchanged."""
+    cfg = WIDE_TINY
+    oc, _, _, z, x0, feat = setup(cfg, B=3)
+    p = O.init_params(oc, 0)
+    h = EcnfHandle(cfg, p, 0)
+    x0 = x0.copy()
+    x0[1] *= 1000.0            # |r|^2 ~ 1e6 into phi_e.0: pre-activations beyond fp16
+    eps = np.random.default_rng(6).standard_normal(x0.shape).astype(np.float32)
+    opts = SolveOptions("euler", 0.5)
+    _, dl_raw, _, st = h.integrate(g(x0), g(feat, torch.int32), 0.0, 1.0, opts, divergence=_lib.DIV_HUTCHINSON,
+                                   eps=g(eps), check_status=False)
+    st = st.cpu().numpy()
+    assert st[0] == 0 and st[2] == 0 and st[1] == _lib.ECNF_E_NONFINITE, st
+    x1, dl, _, st2 = h.integrate(g(x0), g(feat, torch.int32), 0.0, 1.0, opts, divergence=_lib.DIV_HUTCHINSON,
+                                 eps=g(eps))
+    assert (st2.cpu().numpy() == 0).all() and torch.isfinite(dl).all()
+    assert torch.equal(dl[[0, 2]], dl_raw[[0, 2]])
+    _, lq64, _ = O.sample_and_log_prob(p, oc, x0, feat, eps=eps, approx=True, solver="euler", dt0=0.5,
+                                       dtype=np.float64)
+    _, lq32, _ = O.sample_and_log_prob(p, oc, x0, feat, eps=eps, approx=True, solver="euler", dt0=0.5,
+                                       dtype=np.float32)
+    lq = (h.base_log_prob(g(x0)) - dl).cpu().numpy()
+    C = 4.0
+    assert np.abs(lq - lq64).max() <= C * np.abs(lq32 - lq64).max() + 1e-5 * max(1.0, np.abs(lq64).max())
