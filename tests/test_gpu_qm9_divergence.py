@@ -165,3 +165,23 @@ def test_wide_nonfinite_divergence_reruns_on_strict_fp32():
     lq = (h.base_log_prob(g(x0)) - dl).cpu().numpy()
     C = 4.0
     assert np.abs(lq - lq64).max() <= C * np.abs(lq32 - lq64).max() + 1e-5 * max(1.0, np.abs(lq64).max())
+
+
+def test_wide_fp32_adaptive_sample_and_log_prob():
+    """sample_and_log_prob_cnf with the reference's default adaptive solve (Dopri5 + PID, rtol = atol = 1e-5) through
+    the strict-fp32 M = 256 tangent kernels: the PID step sequence is chaotic in fp32, so (as test_gpu_parity's adaptive
+    cases) the end point must land within the spread of the oracle's fp32 adaptive solves, and NFE within 30 %."""
+    cfg = WIDE_TINY
+    oc, params, h, z, x0, feat = setup_prec(cfg, 2, "fp32")
+    x1, dl, nfe, st = h.integrate(g(x0), g(feat, torch.int32), 0.0, 1.0, SolveOptions("dopri5", None),
+                                  divergence=_lib.DIV_HUTCHINSON, eps=g(z))
+    assert int(st.abs().sum()) == 0
+    x64, lq64, nfe64 = O.sample_and_log_prob(params, oc, x0, feat, eps=z, approx=True, solver="dopri5", dt0=None,
+                                             dtype=np.float64)
+    x32, lq32, _ = O.sample_and_log_prob(params, oc, x0, feat, eps=z, approx=True, solver="dopri5", dt0=None,
+                                         dtype=np.float32)
+    spread = max(float(np.abs(x32 - x64).max()), 1e-6)
+    assert float(np.abs(x1.cpu().numpy() - x64).max()) <= 2 * spread + 2e-4
+    lq = (h.base_log_prob(g(x0)) - dl).cpu().numpy()
+    assert float(np.abs(lq - lq64).max()) <= 2 * max(float(np.abs(lq32 - lq64).max()), 1e-6) + 2e-3
+    assert abs(float(nfe.float().mean()) - float(np.mean(nfe64))) <= 0.3 * float(np.mean(nfe64))
