@@ -977,7 +977,7 @@ int ecnf_create(const ecnf_cfg* cfg, const float* params, size_t n_floats, int d
       w.Wh_sn0 = reinterpret_cast<const unsigned*>(dbuf + o.Wh_sn0);
       w.hinv_n0 = o.hinv_n0;
       w.W1_s = reinterpret_cast<const unsigned*>(dbuf + o.W1_s);
-      w.bnp_u = dbuf + o.bnp_u;
+      w.bnp_u = ECNF_FUSED_P ? dbuf + o.bnp_u : nullptr;
       w.w1inv = o.w1inv;
       w.Ws3 = reinterpret_cast<const unsigned*>(dbuf + o.Ws3);
     }
