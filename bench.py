@@ -114,6 +114,16 @@ def _read_durations(d):
     return out
 
 
+def under_profiler() -> str:
+    """Why this process looks profiled ('' when it does not): the rocprofiler tool library in LD_PRELOAD, or the
+    ROCP_* / ROCPROF_* variables rocprofv3 sets for its child."""
+    pre = os.environ.get("LD_PRELOAD", "")
+    if "rocprof" in pre:
+        return "LD_PRELOAD names a rocprofiler library"
+    keys = sorted(k for k in os.environ if k.startswith(("ROCP_", "ROCPROF")))
+    return f"{keys[0]} is set" if keys else ""
+
+
 def collect_pmc(child_args, timeout_s=150):
     """HBM traffic, effective clock and MFMA-pipe occupancy of the dominant kernel, measured in this bench run: the
     same workload is launched by a child `bench.py --pmc-child` under rocprofv3, one counter pass per group of
@@ -127,6 +137,12 @@ def collect_pmc(child_args, timeout_s=150):
     import signal
     import statistics
     import tempfile
+    why = under_profiler()
+    if why:
+        # rocprofv3 is a `#!/usr/bin/env python3` script: started from a process the profiler's tool library has
+        # already attached to, it is an exec of a GPU-initialised process (refused on this pool)
+        print(f"[bench] PMC passes skipped: this process runs under a profiler ({why})", file=sys.stderr, flush=True)
+        return None
     prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
     if not os.path.exists(prof):
         return None

@@ -1144,9 +1144,9 @@ int ecnf_integrate(ecnf_handle* h, const ecnf_solve_opts* o, const float* y0, co
                    float* y1, float* dlogp, int32_t* nfe, int32_t* status, int32_t batch, void* stream) {
   if (!h || !o) return fail(ECNF_E_INVALID, "NULL handle/options");
   if (batch < 0) return fail(ECNF_E_INVALID, "batch < 0");
-  // the handle's arena (ecnf_reserve_workspace) when it is large enough, else the uncached form (same results)
-  return integrate_impl(h, o, y0, feat, eps, y1, dlogp, nfe, status, batch, h->arena, h->arena_bytes,
-                        (hipStream_t)stream, true);
+  // the handle's arena (ecnf_reserve_workspace) when it is large enough, else the uncached form (same results);
+  // integrate_impl reads the arena under its mutex
+  return integrate_impl(h, o, y0, feat, eps, y1, dlogp, nfe, status, batch, nullptr, 0, (hipStream_t)stream, true);
 }
 
 }  // extern "C"
@@ -1192,6 +1192,14 @@ int integrate_impl(ecnf_handle* h, const ecnf_solve_opts* o, const float* y0, co
   sp.pcache = nullptr;
   sp.pcache_slots = 0;
   const size_t need = sp.sparse1 ? pcache_floats(h, batch) : 0;
+  // the arena pointer and size are read under arena_mu, and the lock is held through the dispatch that uses them:
+  // an ecnf_reserve_workspace on another thread cannot free the arena between the read and the launch
+  std::unique_lock<std::mutex> lk(h->arena_mu, std::defer_lock);
+  if (arena && need) {
+    lk.lock();
+    ws = h->arena;
+    ws_bytes = h->arena_bytes;
+  }
   const bool cached = sp.sparse1 && h->exact_form == ECNF_EXACT_FORM_DEFAULT && ws && ws_bytes >= need * sizeof(float);
   if (cached) {
     sp.pcache = ws;
@@ -1201,7 +1209,7 @@ int integrate_impl(ecnf_handle* h, const ecnf_solve_opts* o, const float* y0, co
   if (cached && arena) {
     // the arena is shared by every ecnf_integrate call on the handle: calls on different streams are ordered
     // through an event (no host synchronisation), and the bookkeeping is guarded for calls from several threads
-    std::lock_guard<std::mutex> lk(h->arena_mu);
+    // (arena_mu, held since the arena was read)
     if (!h->arena_ev) HIP_TRY(hipEventCreateWithFlags(&h->arena_ev, hipEventDisableTiming));
     if (h->arena_used && h->arena_stream != stream) HIP_TRY(hipStreamWaitEvent(stream, h->arena_ev, 0));
     HIP_TRY(dispatch_integrate(h, NT, sp, y0, feat, eps, y1, dlogp, nfe, status, batch, stream));

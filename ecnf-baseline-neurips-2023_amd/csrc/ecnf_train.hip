@@ -772,7 +772,9 @@ struct ecnf_trainer {
   std::vector<float*> xc, hin, h1, Ps, Pr, r, len, px, gate, hcat;   // [K] (xc: [K + 1])
   std::vector<float*> ze, ae, zx, ax, zh, ah;                        // [K * L], [K * (L + 1)]
   float *dA, *dB, *dm_gate, *de, *dpx, *dr, *dPs, *dPr, *dhcat, *dh1, *dhin, *dhA, *dhB, *dhn, *red;
-  size_t red_floats;   // partial arena of the deferred split reductions
+  size_t red_floats;   // partial arena of the deferred split reductions (in use)
+  size_t red_capacity; // allocated floats of red
+  size_t red_min;      // the embedding gradient's row-chunk partials
 };
 
 namespace {
@@ -800,6 +802,8 @@ struct Launcher {
   std::vector<RedEntry> pending;
   size_t red_used = 0;   // floats of tr->red in use by pending partials
 
+  // every caller asks for at most tr->red_floats (gemm_wgrad sizes S to it; the embedding partials are part of the
+  // arena's minimum), so after a flush the request fits
   float* red_alloc(size_t floats) {
     if (red_used + floats > tr->red_floats) flush();
     float* p = tr->red + red_used;
@@ -841,8 +845,11 @@ struct Launcher {
       launch(true, false, g, dim3(nblk(N, GT), nblk(M, GT), 1));
       return;
     }
-    float* P = red_alloc((size_t)S * n);
-    float* Pb = db ? red_alloc((size_t)S * N) : nullptr;
+    // P and Pb come from ONE reservation: a flush between two separate calls would reset the arena while P is not
+    // yet deferred, and Pb (or a later partial) could then land on P's region before P is reduced
+    const size_t np = ((size_t)S * n + 63) & ~size_t(63);
+    float* P = red_alloc(np + (db ? (size_t)S * N : 0));
+    float* Pb = db ? P + np : nullptr;
     GemmArgs g{M, N, K, A, lda, dZ, ldz, P, N, 1.0f, nullptr, nullptr, 0, nullptr, 0, nullptr, 0, 0, S, n,
                db, Pb, sqA};
     launch(true, false, g, dim3(nblk(N, GT), nblk(M, GT), S));
@@ -928,6 +935,8 @@ int ecnf_trainer_create(const ecnf_cfg* cfg, int32_t max_batch, int device, ecnf
   tr->red_floats = (size_t)std::max<long>({128 * (std::max((M + H) * M, (H + T) * H) + std::max(M + H, H + T) + 256),
                                            ((BN + 63) / 64) * (long)c.n_features * H + 64, 32L << 20});
   add(&tr->red, (long)tr->red_floats);
+  tr->red_capacity = tr->red_floats;
+  tr->red_min = (size_t)(((BN + 63) / 64) * (long)c.n_features * H + 64);
   size_t total = 0;
   for (auto& q : plan) total += (size_t)q.second;
   tr->arena_floats = total;
@@ -957,6 +966,13 @@ int ecnf_trainer_destroy(ecnf_trainer* tr) {
   TR_TRY(hipDeviceSynchronize());
   TR_TRY(hipFree(tr->arena));
   delete tr;
+  return ECNF_OK;
+}
+
+int ecnf_trainer_set_reduction_arena(ecnf_trainer* tr, size_t floats, size_t* used) {
+  if (!tr) return fail(ECNF_E_INVALID, "NULL trainer");
+  tr->red_floats = floats == 0 ? tr->red_capacity : std::min(tr->red_capacity, std::max(tr->red_min, floats));
+  if (used) *used = tr->red_floats;
   return ECNF_OK;
 }
 

@@ -26,7 +26,7 @@ EXPORTED_SYMBOLS = (
     "ecnf_molecules_per_workgroup", "ecnf_chain_arithmetic", "ecnf_target_log_prob", "ecnf_lse_partials",
     "ecnf_set_precision", "ecnf_get_precision", "ecnf_trainer_create", "ecnf_trainer_destroy", "ecnf_fm_loss_grad",
     "ecnf_adam_update", "ecnf_update_params", "ecnf_integrate_workspace_size", "ecnf_integrate_ws",
-    "ecnf_reserve_workspace", "ecnf_set_exact_form", "ecnf_struct_layout",
+    "ecnf_reserve_workspace", "ecnf_set_exact_form", "ecnf_struct_layout", "ecnf_trainer_set_reduction_arena",
 )
 
 TARGET_LJ, TARGET_DW = 0, 1
@@ -146,6 +146,7 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
         "ecnf_get_precision": ([P, ctypes.POINTER(I32)], ctypes.c_int),
         "ecnf_trainer_create": ([ctypes.POINTER(EcnfCfg), I32, ctypes.c_int, ctypes.POINTER(P)], ctypes.c_int),
         "ecnf_trainer_destroy": ([P], ctypes.c_int),
+        "ecnf_trainer_set_reduction_arena": ([P, SZ, ctypes.POINTER(SZ)], ctypes.c_int),
         "ecnf_fm_loss_grad": ([P, P, P, P, P, P, ctypes.c_float, I32, P, P, P], ctypes.c_int),
         "ecnf_adam_update": ([P, P, P, P, P, P, SZ, ctypes.POINTER(EcnfAdamOpts), P, P], ctypes.c_int),
         "ecnf_update_params": ([P, P, I32], ctypes.c_int),

@@ -18,6 +18,7 @@ Differences, all deliberate and documented in DESIGN.md:
 from __future__ import annotations
 
 import hashlib
+import weakref
 from functools import partial
 from typing import Callable, Mapping, NamedTuple, Optional, Sequence, Tuple, Union
 
@@ -26,8 +27,7 @@ import torch
 
 from . import _lib
 from .engine import EcnfHandle, SolveOptions
-from .params import (CNFConfig, flatten_params, init_from_spec, init_params, kernel_config, pad_params,
-                     ref_param_spec)
+from .params import CNFConfig, flatten_params, init_from_spec, init_params, kernel_config, ref_param_spec
 
 Params = Union[Mapping, np.ndarray, EcnfHandle]
 
@@ -86,7 +86,10 @@ def device_params(params: Params, cfg: CNFConfig, device: torch.device) -> EcnfH
     _HANDLE_CACHE[key] = h
     # a caller that changes this handle (update_params / set_precision, e.g. on the handle of cnf.to_device(p) in a
     # training loop) takes it out of the cache: a later apply(p, ...) uploads p again instead of using other weights
-    h._on_mutate.append(lambda: _HANDLE_CACHE.pop(key, None) if _HANDLE_CACHE.get(key) is h else None)
+    # (a weak reference: a callback holding h would keep every cached handle in a reference cycle, so an evicted
+    # handle's device memory would wait for the cyclic GC instead of being freed when its last caller drops it)
+    ref = weakref.ref(h)
+    h._on_mutate.append(lambda: _HANDLE_CACHE.pop(key, None) if _HANDLE_CACHE.get(key) is ref() else None)
     return h
 
 
@@ -120,7 +123,9 @@ def build_cnf(n_frames: int, dim: int, sigma_min: float, base_scale: float, n_bl
 
     Any mlp_units (each <= 256, a compiled depth) and n_invariant_feat_hidden run on the compiled kernel shape
     params.kernel_config picks: the reference-shaped params are zero-padded on upload (params.pad_params), which
-    leaves the function unchanged.  ``cfg`` is that kernel shape; ``init`` returns reference-shaped params."""
+    leaves the function unchanged.  ``cfg`` is that kernel shape (with the reference widths in ``cfg.ref_mlp_units`` /
+    ``cfg.ref_hidden``, so EcnfHandle.update_params, the Trainer and dataio pad reference-shaped params too);
+    ``init`` returns reference-shaped params."""
     units = tuple(int(u) for u in mlp_units)
     H = int(n_invariant_feat_hidden)
     cfg = kernel_config(int(n_frames), int(dim), int(n_features), H, int(time_embedding_dim), units,
@@ -136,8 +141,7 @@ def build_cnf(n_frames: int, dim: int, sigma_min: float, base_scale: float, n_bl
                               int(seed))
 
     def to_device(params):
-        if padded and not isinstance(params, (EcnfHandle, np.ndarray)):
-            params = pad_params(params, H, cfg.time_embedding_dim, units, cfg)
+        # reference-shaped params of a padded config are zero-padded by flatten_params (cfg.ref_mlp_units)
         return device_params(params, cfg, dev)
 
     def apply(params, x, t, features=None):

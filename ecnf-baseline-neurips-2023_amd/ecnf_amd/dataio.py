@@ -26,9 +26,11 @@ PathLike = Union[str, os.PathLike]
 # weights
 # ---------------------------------------------------------------------------------------------------------------
 def save_params_npz(path: PathLike, params: Mapping, cfg: CNFConfig) -> None:
-    """Write ``params`` (flat flax-path dict or nested flax tree) as an ``.npz`` keyed by flax path (fp32)."""
-    blob = flatten_params(params, cfg)   # validates names and shapes
-    np.savez(path, **unflatten_params(blob, cfg))
+    """Write ``params`` (flat flax-path dict or nested flax tree) as an ``.npz`` keyed by flax path (fp32).  For a
+    padded kernel config (params.kernel_config) the file holds the reference network's shapes, whether ``params`` are
+    reference-shaped or padded."""
+    blob = flatten_params(params, cfg)   # validates names and shapes (pads reference-shaped params)
+    np.savez(path, **unflatten_params(blob, cfg, reference_shapes=True))
 
 
 def load_params_npz(path: PathLike, cfg: CNFConfig) -> dict:

@@ -132,7 +132,11 @@ def main(argv=None) -> None:
     ap.add_argument("--n", type=int, default=0, help="first n molecules of the data (0 = all)")
     ap.add_argument("--batch-size", type=int, default=64)
     ap.add_argument("--approx", action="store_true", help="Hutchinson instead of the exact trace")
-    ap.add_argument("--step-size", type=float, default=0.0, help="> 0: fixed-step Euler, else Dopri5 + PID")
+    ap.add_argument("--step-size", type=float, default=0.0,
+                    help="> 0: fixed steps of this size (the reference's use_fixed_step_size: Dopri5 with a constant "
+                         "dt0, sample_and_log_prob.py:84-85), else Dopri5 + PID")
+    ap.add_argument("--solver", choices=("dopri5", "euler"), default="dopri5",
+                    help="fixed-step solver (euler: NFE = 1 / step size; not the reference's)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--params", default="", help="flax-path .npz (dataio.load_params_npz)")
     ap.add_argument("--dist-backend", default="nccl")
@@ -159,7 +163,9 @@ def main(argv=None) -> None:
     feats = (np.arange(cfg.n_nodes, dtype=np.int32) if args.config == "aldp"     # data.py:146
              else np.zeros(cfg.n_nodes, np.int32))
     h = EcnfHandle(cfg, params, local)
-    opts = (SolveOptions("euler", args.step_size) if args.step_size > 0 else SolveOptions("dopri5", None))
+    if args.solver == "euler" and args.step_size <= 0:
+        ap.error("--solver euler needs --step-size > 0")
+    opts = (SolveOptions(args.solver, args.step_size) if args.step_size > 0 else SolveOptions("dopri5", None))
     target = None
     if args.config == "lj13":
         target = lambda y: T.lj_log_prob(y, cfg.n_nodes, cfg.dim)

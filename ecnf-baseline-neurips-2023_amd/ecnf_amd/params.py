@@ -26,6 +26,11 @@ class CNFConfig:
     base_scale: float = 1.0
     sigma_min: float = 0.01
     normalization_constant: float = 1.0
+    # the reference network's widths when this (kernel) shape zero-pads them (kernel_config); () / 0: not padded.
+    # flatten_params pads reference-shaped params onto this shape by itself, so every entry point that takes params
+    # (EcnfHandle, update_params, the Trainer, dataio) accepts them
+    ref_mlp_units: Tuple[int, ...] = ()
+    ref_hidden: int = 0
 
     @property
     def event_dim(self) -> int:
@@ -96,9 +101,20 @@ def _flat_lookup(params: Mapping) -> Dict[str, np.ndarray]:
     return out
 
 
+def _reference_shaped(flat: Mapping, cfg: CNFConfig) -> bool:
+    """Whether `flat` holds the reference-shaped tree of a padded kernel config (every shape of ref_param_spec)."""
+    if not cfg.ref_mlp_units:
+        return False
+    spec = ref_param_spec(cfg.n_features, cfg.ref_hidden, cfg.time_embedding_dim, cfg.ref_mlp_units, cfg.n_blocks)
+    return all(path in flat and np.asarray(flat[path]).shape == shape for path, shape in spec)
+
+
 def flatten_params(params: Mapping, cfg: CNFConfig) -> np.ndarray:
-    """Flat fp32 blob in ravel_pytree order; raises ValueError on a missing key or a wrong shape."""
+    """Flat fp32 blob in ravel_pytree order; raises ValueError on a missing key or a wrong shape.  For a padded
+    kernel config (kernel_config), reference-shaped params are zero-padded first (pad_params)."""
     flat = _flat_lookup(params)
+    if _reference_shaped(flat, cfg):
+        flat = pad_params(flat, cfg.ref_hidden, cfg.time_embedding_dim, cfg.ref_mlp_units, cfg)
     chunks = []
     for path, shape in param_spec(cfg):
         if path not in flat:
@@ -110,7 +126,11 @@ def flatten_params(params: Mapping, cfg: CNFConfig) -> np.ndarray:
     return np.ascontiguousarray(np.concatenate(chunks))
 
 
-def unflatten_params(blob: np.ndarray, cfg: CNFConfig) -> Dict[str, np.ndarray]:
+def unflatten_params(blob: np.ndarray, cfg: CNFConfig, reference_shapes: bool = False) -> Dict[str, np.ndarray]:
+    """Flat blob -> flax-path dict of cfg's (kernel) shapes; reference_shapes=True crops a padded config's params back
+    to the reference network's shapes (crop_params)."""
+    if reference_shapes and cfg.ref_mlp_units:
+        return crop_params(unflatten_params(blob, cfg), cfg)
     out, off = {}, 0
     for path, shape in param_spec(cfg):
         n = int(np.prod(shape))
@@ -203,9 +223,12 @@ def kernel_config(n_nodes: int, dim: int, n_features: int, hidden: int, time_emb
     if not fits:
         raise ValueError(f"no compiled kernel for mlp_units={U} (depth {L}, width <= 256) at dim {dim}; compiled "
                          f"(M, L, D): {sorted(COMPILED_SHAPES)}")
-    return CNFConfig(n_nodes=n_nodes, dim=dim, n_features=n_features, hidden=32 * ((int(hidden) + 31) // 32),
+    Hp = 32 * ((int(hidden) + 31) // 32)
+    padded = U != (fits[0],) * L or Hp != int(hidden)
+    return CNFConfig(n_nodes=n_nodes, dim=dim, n_features=n_features, hidden=Hp,
                      time_embedding_dim=time_embedding_dim, mlp_width=fits[0], mlp_depth=L, n_blocks=n_blocks,
-                     base_scale=base_scale, sigma_min=sigma_min)
+                     base_scale=base_scale, sigma_min=sigma_min, ref_mlp_units=U if padded else (),
+                     ref_hidden=int(hidden) if padded else 0)
 
 
 def pad_params(params: Mapping, hidden: int, time_embedding_dim: int, mlp_units, kcfg: CNFConfig
@@ -264,4 +287,53 @@ def pad_params(params: Mapping, hidden: int, time_embedding_dim: int, mlp_units,
     out["Embed_0/embedding"] = np.zeros((kcfg.n_features, Hp), np.float32)
     out["Embed_0/embedding"][:, :H] = e
     del hu
+    return out
+
+
+def crop_params(params: Mapping, kcfg: CNFConfig) -> Dict[str, np.ndarray]:
+    """The inverse of pad_params for a padded kernel config: the reference-shaped params (ref_param_spec) read out of
+    the padded ones by the same row / column maps (the padded rows / columns are dropped)."""
+    if not kcfg.ref_mlp_units:
+        return dict(_flat_lookup(params))
+    flat = _flat_lookup(params)
+    H, T, U = kcfg.ref_hidden, kcfg.time_embedding_dim, kcfg.ref_mlp_units
+    Hp, Mp, L = kcfg.hidden, kcfg.mlp_width, len(U)
+    spec = dict(ref_param_spec(kcfg.n_features, H, T, U, kcfg.n_blocks))
+    out: Dict[str, np.ndarray] = {}
+
+    def take(path, rows=None):
+        a = np.asarray(flat[path], np.float32)
+        shape = spec[path]
+        if a.ndim == 0:
+            out[path] = a.reshape(())
+        elif a.ndim == 1:
+            out[path] = a[: shape[0]].copy()
+        elif rows is None:
+            out[path] = a[: shape[0], : shape[1]].copy()
+        else:
+            out[path] = np.concatenate([a[d0:d0 + s1 - s0, : shape[1]] for s0, s1, d0 in rows], axis=0)
+
+    for k in range(kcfg.n_blocks):
+        b = f"EGNN_0/{k}"
+        for nm in ("Dense_0", "Dense_1"):
+            take(f"{b}/{nm}/kernel")
+            take(f"{b}/{nm}/bias")
+        for l in range(L):
+            if l == 0:
+                take(f"{b}/phi_e/Dense_0/kernel", [(0, H, 0), (H, 2 * H, Hp), (2 * H, 2 * H + 1, 2 * Hp)])
+            else:
+                take(f"{b}/phi_e/Dense_{l}/kernel")
+            take(f"{b}/phi_e/Dense_{l}/bias")
+            take(f"{b}/phi_x_torso/Dense_{l}/kernel")
+            take(f"{b}/phi_x_torso/Dense_{l}/bias")
+        for l in range(L + 1):
+            if l == 0:
+                take(f"{b}/phi_h/Dense_0/kernel", [(0, U[-1], 0), (U[-1], U[-1] + H, Mp)])
+            else:
+                take(f"{b}/phi_h/Dense_{l}/kernel")
+            take(f"{b}/phi_h/Dense_{l}/bias")
+        take(f"EGNN_0/Dense_{k}/kernel", [(0, H, 0), (H, H + T, Hp)])
+        take(f"EGNN_0/Dense_{k}/bias")
+    take("EGNN_0/final_scaling")
+    take("Embed_0/embedding")
     return out

@@ -61,6 +61,13 @@ class Trainer:
     def _stream(self) -> int:
         return torch.cuda.current_stream(self.device).cuda_stream
 
+    def set_reduction_arena(self, floats: int = 0) -> int:
+        """Diagnostic (ecnf_trainer_set_reduction_arena): shrink the split-reduction partial arena (0 restores it);
+        returns the size in floats now in use."""
+        used = ctypes.c_size_t()
+        _lib.check(self.lib.ecnf_trainer_set_reduction_arena(self._h, int(floats), ctypes.byref(used)))
+        return used.value
+
     def device_params(self, params) -> torch.Tensor:
         """A flax-path dict, nested flax tree, host blob or device tensor -> the flat fp32 device blob."""
         if torch.is_tensor(params):

@@ -211,6 +211,12 @@ typedef struct ecnf_trainer ecnf_trainer;
 int ecnf_trainer_create(const ecnf_cfg* cfg, int32_t max_batch, int device, ecnf_trainer** out);
 int ecnf_trainer_destroy(ecnf_trainer* tr);
 
+/* Diagnostic: shrink the partial arena of the step's deferred split reductions to `floats` (clamped to
+ * [the embedding partials' minimum, the allocated size]; 0 restores the allocated size) and return the size in use
+ * through `used` (may be NULL).  A small arena makes the step flush mid-way and choose fewer K-splits; the
+ * gradient agrees with the default arena to fp32 rounding (tests/test_gpu_train.py). */
+int ecnf_trainer_set_reduction_arena(ecnf_trainer* tr, size_t floats, size_t* used);
+
 /* loss[0] = mean((v(x_t, t) - u_t)^2) over batch x N*D with x_t = (1 - (1 - sigma_min) t) x0 + t x1,
  * u_t = x1 - (1 - sigma_min) x0 (core.py:35-39); grad = d loss / d params.  x1 (data), x0 (base sample):
  * [batch, N*D]; t: [batch]; feat: [batch, N] (ids must lie in [0, n_features)); loss: DEVICE float[1]. */

@@ -73,6 +73,34 @@ def test_loss_and_grad_match_autograd(name, B):
     assert worst[0][0] <= 1.0, worst[:3]
 
 
+@pytest.mark.parametrize("name,B,floats", [("qm9", 2, 150_000), ("lj13", 8, 60_000), ("lj13", 8, 1)])
+def test_small_reduction_arena(name, B, floats):
+    """A split-reduction arena far below the default (ecnf_trainer_set_reduction_arena) makes the step flush its
+    deferred reductions mid-way, between weight-gradient GEMMs and between a GEMM's weight and bias partials' users
+    (P and Pb are one reservation, so a flush can never recycle P before it is reduced).  The gradient
+    must agree with the default arena's to fp32 rounding (fewer K-splits, another summation order) and with autograd
+    at test_loss_and_grad_match_autograd's tolerance."""
+    cfg = CONFIGS[name]
+    oc, p, x1, x0, t, feat = _case(cfg, B)
+    tr = TR.Trainer(cfg, max_batch=B, device=0)
+    l_def, g_def = tr.loss_and_grad(p, x1, x0, t, feat)
+    used = tr.set_reduction_arena(floats)
+    assert 0 < used < tr.set_reduction_arena(0)
+    tr.set_reduction_arena(floats)
+    l_small, g_small = tr.loss_and_grad(p, x1, x0, t, feat)
+    tr.set_reduction_arena(0)
+    assert torch.isfinite(g_small).all()
+    assert abs(float(l_small) - float(l_def)) <= 1e-6 * abs(float(l_def))
+    gd, gs = unflatten_params(g_def.cpu().numpy(), cfg), unflatten_params(g_small.cpu().numpy(), cfg)
+    _, g_ref = _ref_grad(oc, p, x1, x0, t, feat)
+    gmax = max(float(np.abs(v).max()) for v in g_ref.values())
+    for path, _ in param_spec(cfg):
+        scale = float(np.abs(gd[path]).max())
+        assert float(np.abs(gs[path] - gd[path]).max()) <= 1e-5 * scale + 1e-7 * gmax, path
+        ref = g_ref[path].reshape(gs[path].shape)
+        assert float(np.abs(gs[path] - ref).max()) <= 1e-4 * float(np.abs(ref).max()) + 1e-6 * gmax, path
+
+
 def test_step_is_deterministic_and_batch_bounds():
     cfg = CONFIGS["lj13"]
     oc, p, x1, x0, t, feat = _case(cfg, 8)

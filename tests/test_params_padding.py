@@ -46,3 +46,24 @@ def test_unsupported_shapes_are_refused():
         p = O.init_params(oc, 0)
         del p["EGNN_0/0/phi_e/Dense_1/kernel"]
         P.pad_params(p, 32, 8, (16, 16), P.kernel_config(5, 3, 1, 32, 8, (16, 16), 2))
+
+
+def test_padded_config_entry_points_take_reference_params(tmp_path):
+    """a padded kernel config carries the reference widths (ref_mlp_units / ref_hidden), so every entry
+    point that flattens params (EcnfHandle, update_params, the Trainer, dataio) takes reference-shaped params, and
+    crop_params / unflatten_params(reference_shapes=True) give them back."""
+    from ecnf_amd import dataio
+    units, H, T, K, n = (48, 80), 40, 8, 2, 7
+    oc = O.CNFConfig(n_nodes=n, dim=3, n_features=2, hidden=H, time_embedding_dim=T, mlp_units=units, n_blocks=K)
+    kc = P.kernel_config(n, 3, 2, H, T, units, K)
+    assert kc.ref_mlp_units == units and kc.ref_hidden == H
+    assert P.kernel_config(5, 3, 1, 64, 8, (128, 128, 128), 3).ref_mlp_units == ()   # unpadded: no reference widths
+    p = O.stress_params(O.init_params(oc, 0), oc)
+    blob = P.flatten_params(p, kc)
+    assert np.array_equal(blob, P.flatten_params(P.pad_params(p, H, T, units, kc), kc))
+    back = P.unflatten_params(blob, kc, reference_shapes=True)
+    assert set(back) == set(p) and all(np.array_equal(back[k], p[k]) for k in p)
+    f = tmp_path / "w.npz"
+    dataio.save_params_npz(f, P.pad_params(p, H, T, units, kc), kc)
+    loaded = dataio.load_params_npz(f, kc)
+    assert all(loaded[k].shape == np.asarray(p[k]).shape and np.array_equal(loaded[k], p[k]) for k in p)

@@ -7,7 +7,7 @@ cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 OUT="$GRAFT_REPO_ROOT/gpurun_out/prof_$TAG"
 mkdir -p "$OUT"
-B="bench.py --steps 3 --warmup 1 --cpu-molecules 0 --fp32-steps 0 --train-steps 0"
+B="bench.py --steps 3 --warmup 1 --cpu-molecules 0 --fp32-steps 0 --train-steps 0 --ref-latency-samples 0 --pmc 0"
 # the kernel trace keeps the bench's Hutchinson log-prob leg (its tangent integrate_kernel<4, 1, ...> gets its own
 # stats row); the counter passes profile the primal launches alone
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o run --output-format csv -- python3 $B > "$OUT/kt.log" 2>&1 || exit $?
