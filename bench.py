@@ -415,11 +415,12 @@ def main():
                    "mean_log_q": float(mean_lq), "status_ok": bool(int((st != 0).sum()) == 0)}
         if args.dump:
             os.makedirs(args.dump, exist_ok=True)
-            np.savez(os.path.join(args.dump, f"rank{rank}.npz"), lo=lo, hi=hi, x1=y1.cpu().numpy(),
+            np.savez(os.path.join(args.dump, f"rank{rank}.npz"), lo=lo, hi=hi, z=z.cpu().numpy(),
+                     x0=x0.cpu().numpy(), x1=y1.cpu().numpy(),
                      x1_lp=x1.cpu().numpy(), log_q=log_q.cpu().numpy(), log_w=log_w.cpu().numpy(),
                      rev_ess=float(rev), mean_log_q=float(mean_lq), world=world)
 
-    # the reference's own timing script (examples/load_checkpoint_measure_sampling_time.py:104-126): qm9.yaml
+    # the reference's own timing script (examples/load_checkpoint_measure_sampling_time.py:101-119): qm9.yaml
     # network, ONE molecule per sample_cnf call with the default adaptive solve (Dopri5 + PIDController rtol = atol =
     # 1e-5), 10 calls of which the first is the warm-up; wall time per call incl. the host round trip.  Random-init
     # weights (the script loads a trained wandb checkpoint, unavailable offline), so the step count differs.
@@ -431,21 +432,34 @@ def main():
         gq = torch.Generator(device=dev)
         gq.manual_seed(0)
         fq = torch.zeros((1, qcfg.n_nodes), device=dev, dtype=torch.int32)
-        times, nfes = [], []
-        for i in range(args.ref_latency_samples):
-            zq = torch.randn((1, qcfg.event_dim), generator=gq, device=dev)
-            torch.cuda.synchronize(dev)
-            t1 = time.perf_counter()
-            xq, _, nq, sq = hq.integrate(hq.base_sample(zq), fq, 0.0, 1.0, SolveOptions("dopri5", None))
-            xq.cpu()                                   # the sample reaches the host, as jax's result does
-            if i:
-                times.append(time.perf_counter() - t1)
-                nfes.append(int(nq.max()))
+
+        def calls(team_mode):
+            # team_mode 0: the default (team mode: ecnf_team_workgroups(1) workgroups per molecule); 1: the batch path
+            hq.set_team(team_mode)
+            gq.manual_seed(0)
+            times, nfes, xs = [], [], []
+            for i in range(args.ref_latency_samples):
+                zq = torch.randn((1, qcfg.event_dim), generator=gq, device=dev)
+                torch.cuda.synchronize(dev)
+                t1 = time.perf_counter()
+                xq, _, nq, sq = hq.integrate(hq.base_sample(zq), fq, 0.0, 1.0, SolveOptions("dopri5", None))
+                xs.append(xq.cpu())                    # the sample reaches the host, as jax's result does
+                if i:
+                    times.append(time.perf_counter() - t1)
+                    nfes.append(int(nq.max()))
+            hq.set_team(0)
+            return times, nfes, xs
+
+        G = hq.team_workgroups(1)
+        times, nfes, xs = calls(0)
+        times_b, _, xs_b = calls(1)
         del hq
         return {"workload": "qm9 sample_cnf, 1 molecule per call, Dopri5 + PID rtol=atol=1e-5 "
-                            "(load_checkpoint_measure_sampling_time.py:104-126), random-init weights",
+                            "(load_checkpoint_measure_sampling_time.py:101-119), random-init weights",
                 "ms_median": 1e3 * float(np.median(times)), "ms_min": 1e3 * float(np.min(times)),
-                "nfe_median": float(np.median(nfes)), "calls": len(times)}
+                "nfe_median": float(np.median(nfes)), "calls": len(times), "team_workgroups": G,
+                "batch_path_ms_median": 1e3 * float(np.median(times_b)),
+                "team_equals_batch_path": all(bool(torch.equal(a, b)) for a, b in zip(xs, xs_b))}
 
     if world == 1 and args.ref_latency_samples > 1:
         try:   # an auxiliary leg: its failure is reported in the line, never fails the headline measurement

@@ -264,6 +264,17 @@ struct ecnf_handle {
   hipEvent_t arena_ev;
   bool arena_used;
   hipStream_t arena_stream;
+  // team (latency) mode of the primal kernels (egnn_eval.hpp team_exchange): exchange slots and the per-molecule
+  // arrival counters / timeout flags, allocated at create for up to team_cap molecules of team_gcap workgroups;
+  // shared by every ecnf_integrate on the handle (ordered across streams by team_ev under team_mu)
+  int team_mode;        // ecnf_set_team: 0 auto, 1 off, G >= 2 forced
+  int team_cap, team_gcap, team_slot;
+  float* team_buf;
+  unsigned* team_sync;  // [team_cap] counters, then [team_cap] timeout flags (one 16-B-padded block, zeroed per launch)
+  std::mutex team_mu;
+  hipEvent_t team_ev;
+  bool team_used;
+  hipStream_t team_stream;
 };
 
 namespace {
@@ -402,6 +413,13 @@ struct HostBlock {
   const float *tb[4], *tk[4];
   const float *nb, *nk;
 };
+
+// team mode (team_size): molecules per launch, and the bytes of the counter / timeout block (16-B multiple)
+constexpr int kTeamCap = 32;
+constexpr size_t kTeamSyncBytes = 2 * kTeamCap * sizeof(unsigned);
+
+// waves per workgroup of the primal kernels (Geo<NF, 0, P>::NW)
+int primal_waves(const ecnf_cfg& c) { return c.mlp_width <= 128 ? 8 : 4; }
 
 // Geo<NF, NT, P>::kSplit: the split primal kernels (16-B node-row strides, stored segment parts)
 bool split_primal(const ecnf_cfg& c, int NT, int P) {
@@ -555,12 +573,52 @@ Net net_for_batch(const ecnf_handle* h, int ix, int B, size_t* lds, bool adaptiv
   return n;
 }
 
-hipError_t dispatch_integrate(const ecnf_handle* h, int NT, const SolveP& sp, const float* y0, const int32_t* feat,
+// Team (latency) mode: G workgroups per molecule (egnn_eval.hpp team_exchange) for the primal kernels when the batch
+// leaves most CUs idle.  Auto: one edge-tile round per block (G = ceil(tiles per molecule / waves)) where a round is
+// long against the ~5 us exchange (M = 256: QM9's 36-60 us rounds), B G <= CUs (one member per CU is always
+// co-resident) and B <= team_cap.  ecnf_set_team forces G (>= 2) or turns it off (1).
+int team_size(const ecnf_handle* h, int NT, int B) {
+  const ecnf_cfg& c = h->cfg;
+  if (NT != 0 || B < 1 || B > h->team_cap || h->team_mode == 1 ||
+      !team_shape(c.mlp_width, NT, c.mlp_depth, c.dim, h->prec))
+    return 1;
+  const int tpm = h->net[0].EP / 32;
+  int G;
+  if (h->team_mode >= 2) {
+    G = std::min(std::min(h->team_mode, h->team_gcap), tpm);
+  } else {
+    if (h->cfg.mlp_width < 256) return 1;
+    G = std::min((tpm + primal_waves(h->cfg) - 1) / primal_waves(h->cfg), h->team_gcap);
+  }
+  if (G < 2 || (long)B * G > h->ncu) return 1;
+  return G;
+}
+
+hipError_t dispatch_integrate(const ecnf_handle* h, int NT, const SolveP& sp_in, const float* y0, const int32_t* feat,
                               const float* eps, float* y1, float* dlogp, int32_t* nfe, int32_t* status, int B,
                               hipStream_t stream) {
   const int M = h->cfg.mlp_width, L = h->cfg.mlp_depth, D = h->cfg.dim, P = h->prec, ix = 2 * P + NT;
   size_t lds = 0;
-  const Net net = net_for_batch(h, ix, B, &lds, sp.adaptive != 0);
+  SolveP sp = sp_in;
+  const int G = team_size(h, NT, B);
+  Net net;
+  if (G > 1) {
+    net = h->net[ix];
+    const int RP = 32 * ((h->cfg.n_nodes + 31) / 32);
+    set_mpw(net, h->cfg, NT, P, 1, RP);
+    lds = lds_bytes(h->cfg, NT, P, 1, RP);
+    net.lds_floats = (int)(lds / 4);
+    sp.team.G = G;
+    sp.team.slot = h->team_slot;
+    sp.team.buf = h->team_buf;
+    sp.team.ctr = h->team_sync;
+    sp.team.timeout = reinterpret_cast<int*>(h->team_sync + kTeamCap);
+    hipError_t e = hipMemsetAsync(h->team_sync, 0, kTeamSyncBytes, stream);
+    if (e != hipSuccess) return e;
+  } else {
+    sp.team = TeamP{};
+    net = net_for_batch(h, ix, B, &lds, sp.adaptive != 0);
+  }
 #define ECNF_CALL(m, l, d, nt, p) \
   launch_integrate<m / 32, nt, l, d, p>(net, lds, sp, y0, feat, eps, y1, dlogp, nfe, status, B, stream)
 #define X(m, l, d)                                                                                           \
@@ -997,6 +1055,21 @@ int ecnf_create(const ecnf_cfg* cfg, const float* params, size_t n_floats, int d
     delete h;
     return fail(ECNF_E_UNSUPPORTED, "configuration does not fit the LDS budget");
   }
+  {
+    // team-mode buffers (team_size): up to kTeamCap molecules of up to team_gcap workgroups each
+    const Net& n = h->net[0];
+    const int tpm = n.EP / 32;
+    h->team_cap = kTeamCap;
+    h->team_gcap = std::min(tpm, std::max(4, (tpm + primal_waves(c) - 1) / primal_waves(c)));
+    h->team_slot = c.n_nodes * M + tpm * M + ((c.n_nodes * c.dim + 3) & ~3);
+    const size_t nb = (size_t)h->team_cap * 2 * h->team_gcap * h->team_slot * sizeof(float);
+    if (hipMalloc(&h->team_buf, nb) != hipSuccess || hipMalloc(&h->team_sync, kTeamSyncBytes) != hipSuccess) {
+      if (h->team_buf) hipFree(h->team_buf);
+      hipFree(dbuf);
+      delete h;
+      return fail(ECNF_E_HIP, "team-mode exchange buffers: out of device memory");
+    }
+  }
   *out = h;
   g_err.clear();
   return ECNF_OK;
@@ -1036,6 +1109,9 @@ int ecnf_destroy(ecnf_handle* h) {
   HIP_TRY(hipFree(h->dbuf));
   if (h->arena) HIP_TRY(hipFree(h->arena));
   if (h->arena_ev) HIP_TRY(hipEventDestroy(h->arena_ev));
+  if (h->team_buf) HIP_TRY(hipFree(h->team_buf));
+  if (h->team_sync) HIP_TRY(hipFree(h->team_sync));
+  if (h->team_ev) HIP_TRY(hipEventDestroy(h->team_ev));
   delete h;
   return ECNF_OK;
 }
@@ -1128,6 +1204,19 @@ int ecnf_set_exact_form(ecnf_handle* h, int32_t form) {
   return ECNF_OK;
 }
 
+int ecnf_set_team(ecnf_handle* h, int32_t mode) {
+  if (!h) return fail(ECNF_E_INVALID, "NULL handle");
+  if (mode < 0) return fail(ECNF_E_INVALID, "team mode must be 0 (auto), 1 (off) or >= 2 workgroups per molecule");
+  h->team_mode = mode;
+  return ECNF_OK;
+}
+
+int ecnf_team_workgroups(ecnf_handle* h, int32_t with_tangent, int32_t batch, int32_t* G) {
+  if (!h || !G) return fail(ECNF_E_INVALID, "NULL argument");
+  *G = team_size(h, with_tangent ? 1 : 0, batch);
+  return ECNF_OK;
+}
+
 int ecnf_integrate_ws(ecnf_handle* h, const ecnf_solve_opts* o, const float* y0, const int32_t* feat, const float* eps,
                       float* y1, float* dlogp, int32_t* nfe, int32_t* status, int32_t batch, void* workspace,
                       size_t workspace_bytes, void* stream) {
@@ -1191,6 +1280,7 @@ int integrate_impl(ecnf_handle* h, const ecnf_solve_opts* o, const float* y0, co
   sp.sparse1 = exact_sparse(h, o->divergence) && h->exact_form != ECNF_EXACT_FORM_ALL_DUAL ? 1 : 0;
   sp.pcache = nullptr;
   sp.pcache_slots = 0;
+  sp.team = TeamP{};   // dispatch_integrate sets it (team_size)
   const size_t need = sp.sparse1 ? pcache_floats(h, batch) : 0;
   // the arena pointer and size are read under arena_mu, and the lock is held through the dispatch that uses them:
   // an ecnf_reserve_workspace on another thread cannot free the arena between the read and the launch
@@ -1216,6 +1306,15 @@ int integrate_impl(ecnf_handle* h, const ecnf_solve_opts* o, const float* y0, co
     HIP_TRY(hipEventRecord(h->arena_ev, stream));
     h->arena_used = true;
     h->arena_stream = stream;
+  } else if (team_size(h, NT, batch) > 1) {
+    // team mode: the exchange slots and counters are shared by every solve on the handle (ordered as the arena)
+    std::lock_guard<std::mutex> tl(h->team_mu);
+    if (!h->team_ev) HIP_TRY(hipEventCreateWithFlags(&h->team_ev, hipEventDisableTiming));
+    if (h->team_used && h->team_stream != stream) HIP_TRY(hipStreamWaitEvent(stream, h->team_ev, 0));
+    HIP_TRY(dispatch_integrate(h, NT, sp, y0, feat, eps, y1, dlogp, nfe, status, batch, stream));
+    HIP_TRY(hipEventRecord(h->team_ev, stream));
+    h->team_used = true;
+    h->team_stream = stream;
   } else {
     HIP_TRY(dispatch_integrate(h, NT, sp, y0, feat, eps, y1, dlogp, nfe, status, batch, stream));
   }

@@ -49,6 +49,9 @@ struct SolveP {
   // pcache_slots: molecule slots the buffer holds (>= grid x MPW; device-checked build: ECNF_DCHECK bit 6)
   float* pcache;
   int pcache_slots;
+  // team (latency) mode of the primal kernels (egnn_eval.hpp team_exchange): team.G > 1 workgroups per molecule,
+  // MPW = 1, grid = batch x G (a cooperative launch: every member co-resident)
+  TeamP team;
 };
 
 // solver state in LDS, after the eval region
@@ -95,9 +98,9 @@ __device__ inline bool check_features(const Net& net, int* f) {
 
 // one evaluation of the joint field g(tau, y) = dir * f(dir * tau, y) at (st.ts, st.ys) for every molecule
 // of the workgroup; writes kx_out [MPW][ND] and kl_out [MPW].  Exactly one egnn_eval call site (it is inlined).
-template <int NF, int NT, int L, int D, int P>
+template <int NF, int NT, int L, int D, int P, bool TEAM>
 __device__ __forceinline__ void joint_field(const Net& net, const Lds& s, const SolverLds& st, const SolveP& sp,
-                                            float* kx_out, float* kl_out) {
+                                            float* kx_out, float* kl_out, const TeamCtx* tm, int* tepoch) {
   constexpr int kThreads = Geo<NF, NT, P>::NTHR;
   const int tid = opaque_tid(), MPW = net.MPW, ND = net.ND;
   // NT == 0: one primal eval; Hutchinson: one JVP along eps; exact: the trace of J from ND - D JVPs along e_k,
@@ -126,8 +129,8 @@ __device__ __forceinline__ void joint_field(const Net& net, const Lds& s, const 
                     ? sp.pcache + (size_t)blockIdx.x * MPW * (net.N * (NF * 32) + 2 * net.N * D)
                     : nullptr;
     ECNF_DCHECK(!pc || (int)(blockIdx.x + 1) * MPW <= sp.pcache_slots, 6);
-    egnn_eval<NF, NT, L, D, P>(net, s, st.ys, st.ts, st.tin, st.vout, st.tout, st.active, sparse ? k / D : -1, pc,
-                               k0 == 0 ? 1 : 2);
+    egnn_eval<NF, NT, L, D, P, TEAM>(net, s, st.ys, st.ts, st.tin, st.vout, st.tout, st.active, sparse ? k / D : -1,
+                                     pc, k0 == 0 ? 1 : 2, tm, tepoch);
     if constexpr (NT) {
       if (tid < MPW) {
         if (sp.div == ECNF_DIV_HUTCHINSON) {
@@ -156,8 +159,9 @@ __device__ inline float rms_state(float sumsq_x, float l, int ND, bool track) {
 
 enum Phase { kEuler = 0, kInit0 = 1, kInit1 = 2, kFsal = 3, kStage = 4 };
 
-// The whole solve as a phase machine around ONE field evaluation per loop trip.
-template <int NF, int NT, int L, int D, int P>
+// The whole solve as a phase machine around ONE field evaluation per loop trip.  TEAM: the team (latency) mode
+// instantiation (egnn_eval.hpp team_exchange; launched only with sp.team.G > 1, compiled for team_shape)
+template <int NF, int NT, int L, int D, int P, bool TEAM = false>
 __global__ __launch_bounds__((Geo<NF, NT, P>::NTHR)) __attribute__((amdgpu_waves_per_eu(Geo<NF, NT, P>::WPE))) void integrate_kernel(Net net, SolveP sp, const float* __restrict__ y0,
                                                                   const int32_t* __restrict__ feat,
                                                                   const float* __restrict__ eps, float* y1,
@@ -168,7 +172,16 @@ __global__ __launch_bounds__((Geo<NF, NT, P>::NTHR)) __attribute__((amdgpu_waves
   const int tid = threadIdx.x, MPW = net.MPW, ND = net.ND, N = net.N;
   const Lds s = carve_lds<NT, Geo<NF, NT, P>::kSplitN, Geo<NF, NT, P>::kNoP>(net, smem);
   const SolverLds st = carve_solver(s.tail, MPW, ND);
-  const int mol0 = blockIdx.x * MPW;
+  // team mode: workgroup blockIdx = T G + r is member r of molecule T's team (MPW = 1); only member 0 writes outputs
+  TeamCtx team_ctx;
+  constexpr bool team = TEAM;
+  team_ctx.p = sp.team;
+  team_ctx.T = team ? (int)blockIdx.x / sp.team.G : 0;
+  team_ctx.r = team ? (int)blockIdx.x - team_ctx.T * sp.team.G : 0;
+  const TeamCtx* tm = team ? &team_ctx : nullptr;
+  int tepoch = 0;
+  const bool writer_wg = team_ctx.r == 0;
+  const int mol0 = team ? team_ctx.T : blockIdx.x * MPW;
   const int nmol = min(MPW, B - mol0);
   const int a = align4(MPW * ND), b = align4(MPW);
   ECNF_DCHECK((int)(s.tail - smem) + solver_lds_floats(MPW, ND) <= net.lds_floats, 0);
@@ -260,7 +273,7 @@ __global__ __launch_bounds__((Geo<NF, NT, P>::NTHR)) __attribute__((amdgpu_waves
     }
     __syncthreads();
 
-    joint_field<NF, NT, L, D, P>(net, s, st, sp, kx_out, kl_out);
+    joint_field<NF, NT, L, D, P, TEAM>(net, s, st, sp, kx_out, kl_out, tm, &tepoch);
 
     // ------------------------------------------------ consume it
     if (phase == kEuler) {
@@ -400,6 +413,14 @@ __global__ __launch_bounds__((Geo<NF, NT, P>::NTHR)) __attribute__((amdgpu_waves
     for (int c = 0; c < ND; ++c) fin = fin && isfinite(st.y[tid * ND + c]);
     if (!fin) st.status[tid] = ECNF_E_NONFINITE;
   }
+  if constexpr (team) {
+    // an exchange that timed out (a member not co-resident) leaves this molecule's results undefined
+    if (tid == 0 && __hip_atomic_load((ECNF_GLOBAL int*)(sp.team.timeout + team_ctx.T), __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT))
+      st.status[0] = ECNF_E_HIP;
+    __syncthreads();
+    if (!writer_wg) return;
+  }
   for (int i = tid; i < nmol * ND; i += kThreads) y1[(size_t)mol0 * ND + i] = st.y[i];
   if (tid < nmol) {
     if (dlogp) dlogp[mol0 + tid] = st.lp[tid];
@@ -455,11 +476,36 @@ __global__ __launch_bounds__((Geo<NF, NT, P>::NTHR)) __attribute__((amdgpu_waves
   }
 }
 
+// shapes with a team-mode kernel (ecnf_hip.hip team_size): the split primal kernels of the BASELINE networks
+// (QM9 M = 256, LJ13 M = 128, ALDP M = 64)
+constexpr bool team_shape(int M, int NT, int L, int D, int P) {
+  return NT == 0 && P == 0 && D == 3 && ((M == 256 && L == 4) || (M == 128 && L == 3) || (M == 64 && L == 2));
+}
+
 // ---- templated launchers (one instantiation per compiled shape and tangent flag) ----
 template <int NF, int NT, int L, int D, int P>
 hipError_t launch_integrate(const Net& net, size_t lds, const SolveP& sp, const float* y0, const int32_t* feat,
                             const float* eps, float* y1, float* dlogp, int32_t* nfe, int32_t* status, int B,
                             hipStream_t stream) {
+  if constexpr (team_shape(NF * 32, NT, L, D, P)) {
+    if (sp.team.G > 1) {
+    // team mode: the G members of a molecule wait on each other, so the launch must be co-resident; the cooperative
+    // launch checks the grid against the occupancy query (hipErrorCooperativeLaunchTooLarge instead of a hang)
+    auto kt = integrate_kernel<NF, NT, L, D, P, true>;
+    hipError_t e = hipFuncSetAttribute((const void*)kt, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    Net n = net;
+    SolveP p = sp;
+    const float* a_y0 = y0;
+    const int32_t* a_feat = feat;
+    const float* a_eps = eps;
+    int a_B = B;
+    void* args[] = {&n, &p, &a_y0, &a_feat, &a_eps, &y1, &dlogp, &nfe, &status, &a_B};
+    return hipLaunchCooperativeKernel((const void*)kt, dim3(B * sp.team.G), dim3(Geo<NF, NT, P>::NTHR), args, lds,
+                                      stream);
+    }
+  }
+  if (sp.team.G > 1) return hipErrorInvalidValue;   // no team kernel for this shape (team_size never asks for one)
   auto k = integrate_kernel<NF, NT, L, D, P>;
   hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;

@@ -509,14 +509,22 @@ __device__ __forceinline__ void node_task(const float* X1, int ldx1, int K1, con
 // shares every A fragment and gets no bias, act'(pre) * (X_T W) (as node_task).
 // INPLACE (Y may alias X1): every wave of the workgroup calls it once (active = false: no task) and the outputs are
 // written after a barrier that follows every wave's k-loop.
-template <int NA, int NT = 0, bool INPLACE = false>
-__device__ __forceinline__ void node_task_split(const float* X1, int ldx1, int K1, const float* X2, int ldx2, int K2,
-                                                const unsigned* __restrict__ Wpk, float winv,
-                                                const float* __restrict__ bias, bool act, const float* resid, int ldr, float* Y, int ldy, int RP,
-                                                int nvalid, int jb, int ct, int lane, bool active = true) {
 #ifndef ECNF_NODE_PFA
 #define ECNF_NODE_PFA 2
 #endif
+// the first ECNF_NODE_PFA k-steps of a node GEMM task's A fragments, loaded before the barrier that precedes the GEMM
+// (node_prefetch): the weights do not depend on the phase's inputs, so their L2 latency overlaps the barrier wait and
+// the previous phase's tail instead of opening every node phase
+struct NodePre {
+  u32x4 w[ECNF_NODE_PFA][2][kPieces];
+};
+
+template <int NA, int NT = 0, bool INPLACE = false, bool PRE = false>
+__device__ __forceinline__ void node_task_split(const float* X1, int ldx1, int K1, const float* X2, int ldx2, int K2,
+                                                const unsigned* __restrict__ Wpk, float winv,
+                                                const float* __restrict__ bias, bool act, const float* resid, int ldr, float* Y, int ldy, int RP,
+                                                int nvalid, int jb, int ct, int lane, bool active = true,
+                                                const NodePre* pre = nullptr) {
   constexpr int PFA = ECNF_NODE_PFA;   // k-steps of A fragments in flight ahead of the MFMAs
   jb = __builtin_amdgcn_readfirstlane(jb);   // uniform: buffer-load offsets in SGPRs (no waterfall loops)
   ct = __builtin_amdgcn_readfirstlane(ct);
@@ -583,7 +591,17 @@ __device__ __forceinline__ void node_task_split(const float* X1, int ldx1, int K
   if (active) {
   bload(0, n, bv);
   if constexpr (NT) bload(0, RP + n, bvT);
-  static_for<PFA>([&](auto Ic) { aload(min((int)decltype(Ic)::value, nks - 1), wa[decltype(Ic)::value]); });
+  if constexpr (PRE) {
+    static_for<PFA>([&](auto Ic) {
+      constexpr int i = decltype(Ic)::value;
+#pragma unroll
+      for (int a = 0; a < NA; ++a)
+#pragma unroll
+        for (int p = 0; p < kPieces; ++p) wa[i][a][p] = pre->w[i][a][p];
+    });
+  } else {
+    static_for<PFA>([&](auto Ic) { aload(min((int)decltype(Ic)::value, nks - 1), wa[decltype(Ic)::value]); });
+  }
   auto kstep = [&](int ks, auto Ic) {
     constexpr int i = decltype(Ic)::value;
     aload(min(ks + PFA, nks - 1), wa[(i + PFA) % S]);
@@ -656,23 +674,69 @@ __device__ __forceinline__ void node_task_split(const float* X1, int ldx1, int K
 // and get no bias, act'(pre) * (X_T W).  Output blocks are paired (shared B reads, two independent MFMA
 // chains) whenever the pairs still give every wave a task.
 // ---------------------------------------------------------------------------------------------------
-template <int NT, int NW, bool SPLIT>
-__device__ __forceinline__ void node_gemm(const float* X1, int ldx1, int K1, const float* X2, int ldx2, int K2,
-                                          const float* __restrict__ W, const unsigned* __restrict__ Ws, float winv,
-                                          int ldw, const float* __restrict__ bias, int NOUT, bool act, const float* resid,
-                                          int ldr, float* Y, int ldy, int RP, int nvalid, int wave, int lane) {
-  const int njb = NOUT >> 5, nct = RP >> 5;
-  if constexpr (SPLIT) {
 #ifndef ECNF_NODE_PAIR_DIV
 #define ECNF_NODE_PAIR_DIV 1
 #endif
-    if ((njb % 2) == 0 && (njb / 2) * nct >= NW / ECNF_NODE_PAIR_DIV) {   // two output blocks per task share the B split
+// split node GEMM task deal: two output blocks per task (sharing the B split) when the pairs still give every wave a
+// task
+template <int NW>
+__device__ __forceinline__ bool node_paired(int njb, int nct) {
+  return (njb % 2) == 0 && (njb / 2) * nct >= NW / ECNF_NODE_PAIR_DIV;
+}
+
+// issue the first PFA k-steps of A fragments of this wave's first task of the split node GEMM (node_gemm's deal) into
+// pre; no task: nothing.  The matching node_gemm<..., PRE = true> call consumes them.
+template <int NW>
+__device__ __forceinline__ void node_prefetch(const unsigned* __restrict__ Ws, int K1, int K2, int NOUT, int RP,
+                                              int wave, int lane, NodePre& pre) {
+  const int njb = NOUT >> 5, nct = RP >> 5;
+  const bool pair = node_paired<NW>(njb, nct);
+  const int ntask = pair ? (njb / 2) * nct : njb * nct;
+  if (wave >= ntask) return;
+  const int jb = __builtin_amdgcn_readfirstlane(pair ? 2 * (wave % (njb / 2)) : wave % njb);
+  const int nks = ((K1 + 15) >> 4) + ((K2 + 15) >> 4);
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned*>(Ws), (short)0,
+                                                                         0x7fffffff, 0x00020000);
+  static_for<ECNF_NODE_PFA>([&](auto Ic) {
+    constexpr int i = decltype(Ic)::value;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+      if (a == 0 || pair)
+#pragma unroll
+        for (int p = 0; p < kPieces; ++p)
+          pre.w[i][a][p] = wload(rsrc, lane * 16, (((jb + a) * nks + min(i, nks - 1)) * kPieces + p) * kPieceBytes);
+  });
+}
+
+template <int NT, int NW, bool SPLIT, bool PRE = false>
+__device__ __forceinline__ void node_gemm(const float* X1, int ldx1, int K1, const float* X2, int ldx2, int K2,
+                                          const float* __restrict__ W, const unsigned* __restrict__ Ws, float winv,
+                                          int ldw, const float* __restrict__ bias, int NOUT, bool act, const float* resid,
+                                          int ldr, float* Y, int ldy, int RP, int nvalid, int wave, int lane,
+                                          const NodePre* pre = nullptr) {
+  const int njb = NOUT >> 5, nct = RP >> 5;
+  if constexpr (SPLIT) {
+    if (node_paired<NW>(njb, nct)) {   // two output blocks per task share the B split
       const int npair = njb / 2;
-      for (int task = wave; task < npair * nct; task += NW)
+      int task = wave;
+      if constexpr (PRE) {   // this wave's first task with its prefetched A fragments (node_prefetch)
+        if (task < npair * nct)
+          node_task_split<2, NT, false, true>(X1, ldx1, K1, X2, ldx2, K2, Ws, winv, bias, act, resid, ldr, Y, ldy, RP,
+                                              nvalid, 2 * (task % npair), task / npair, lane, true, pre);
+        task += NW;
+      }
+      for (; task < npair * nct; task += NW)
         node_task_split<2, NT>(X1, ldx1, K1, X2, ldx2, K2, Ws, winv, bias, act, resid, ldr, Y, ldy, RP, nvalid,
                                2 * (task % npair), task / npair, lane);
     } else {
-      for (int task = wave; task < njb * nct; task += NW)
+      int task = wave;
+      if constexpr (PRE) {
+        if (task < njb * nct)
+          node_task_split<1, NT, false, true>(X1, ldx1, K1, X2, ldx2, K2, Ws, winv, bias, act, resid, ldr, Y, ldy, RP,
+                                              nvalid, task % njb, task / njb, lane, true, pre);
+        task += NW;
+      }
+      for (; task < njb * nct; task += NW)
         node_task_split<1, NT>(X1, ldx1, K1, X2, ldx2, K2, Ws, winv, bias, act, resid, ldr, Y, ldy, RP, nvalid,
                                task % njb, task / njb, lane);
     }
@@ -1589,16 +1653,135 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
 }
 
 // ---------------------------------------------------------------------------------------------------
+// Team (latency) mode: G workgroups integrate ONE molecule together (a batch far below the CU count, e.g. the
+// reference's one-molecule-per-call sampling timer, examples/load_checkpoint_measure_sampling_time.py:101-119).
+// Every member runs the same solver and node phases redundantly (deterministic, so bitwise identical in every
+// member); the molecule's edge tiles are dealt round-robin over the members (tile t -> member t mod G) and, after each
+// block's edge phase, the members exchange their parts of the edge aggregates through global memory:
+//   * message rows (macc) from the member holding the tile where the receiver's segment starts; with stored segment
+//     parts (Net::cross) the continuation rows (cross) from the member holding their tile, else (atomically
+//     accumulated parts) plus the other tile's member's row;
+//   * shift rows (dxacc) from the one or two members holding the receiver's tiles.
+// A receiver's segment touches at most two tiles and a missing part is an exact zero, so the rebuilt aggregates are
+// bitwise those of a single workgroup running every tile: results are bitwise independent of G.
+// Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility; cdna_hip_programming.md Guideline 16 R1): owned rows
+// stored write-through (sc1, 16 B), every storing wave drains (vmcnt(0)), a workgroup barrier, one lane's agent-scope
+// atomic add on the molecule's arrival counter; one lane polls it (relaxed sc1 loads, s_sleep) until all G members
+// arrived for this exchange, one agent-scope acquire, vmcnt(0), barrier, then plain loads.  Slots are double
+// buffered by exchange parity (a member can run at most one exchange ahead of the slowest).  Polls are bounded: a
+// timeout marks the molecule (status ECNF_E_HIP) instead of hanging the grid.
+// ---------------------------------------------------------------------------------------------------
+struct TeamP {
+  int G;               // workgroups per molecule (<= 1: off)
+  int slot;            // floats per exchange slot: N M (messages) + (EP / 32) M (continuation rows) + align4(N D)
+  float* buf;          // [molecules][2][G][slot]
+  unsigned* ctr;       // [molecules] arrival counters (zeroed before every launch)
+  int* timeout;        // [molecules] set when an exchange timed out (zeroed before every launch)
+};
+
+struct TeamCtx {
+  TeamP p;
+  int r;               // this workgroup's rank in its team
+  int T;               // the team's molecule
+};
+
+typedef ECNF_GLOBAL unsigned* gu32_p;
+
+// one exchange of the edge aggregates (MPW = 1; all threads of the workgroup, after the edge phase's barrier)
+template <int NT, int NTHR>
+__device__ __forceinline__ void team_exchange(const Net& net, const Lds& s, const TeamCtx& tm, int epoch) {
+  static_assert(NT == 0, "team mode runs the primal kernels");
+  const int tid = opaque_tid();
+  const int N = net.N, M = net.M, D = net.D, G = tm.p.G, r = tm.r, nn1 = N - 1, SR = net.SR;
+  const int tpm = net.EP >> 5, M4 = M >> 2;
+  const int off_x = N * M, off_d = N * M + tpm * M;
+  float* base = tm.p.buf + ((size_t)tm.T * 2 + (epoch & 1)) * G * tm.p.slot;
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, 0x7fffffff, 0x00020000);
+  const int mine = r * tm.p.slot * 4;   // byte offset of this member's slot
+  auto st16 = [&](int fo, f32x4 v) {   // write-through (sc1) 16-B store of slot float fo
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rsrc, fo * 4, mine, 16);
+  };
+  auto first_tile = [&](int i) { return (i * SR) >> 5; };
+  auto last_tile = [&](int i) { return (i * SR + nn1 - 1) >> 5; };
+  // ---- publish the rows this member owns
+  for (int idx = tid; idx < N * M4; idx += NTHR) {
+    const int i = idx / M4, c = (idx - i * M4) * 4;
+    if (first_tile(i) % G == r) st16(i * M + c, *reinterpret_cast<const f32x4*>(s.macc + i * s.ld_m + c));
+    if (!net.cross && last_tile(i) != first_tile(i) && last_tile(i) % G == r)   // the receiver's second part
+      st16(i * M + c, *reinterpret_cast<const f32x4*>(s.macc + i * s.ld_m + c));
+  }
+  if (net.cross)
+    for (int idx = tid; idx < tpm * M4; idx += NTHR) {
+      const int t = idx / M4, c = (idx - t * M4) * 4;
+      if (t % G == r) st16(off_x + t * M + c, *reinterpret_cast<const f32x4*>(s.cross + t * s.ld_m + c));
+    }
+  for (int idx = tid; idx < (N * D + 3) >> 2; idx += NTHR)   // every member: its whole (partial) shift rows
+    st16(off_d + 4 * idx, *reinterpret_cast<const f32x4*>(s.dxacc + 4 * idx));
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains its write-through stores
+  __syncthreads();
+  // ---- arrive, then wait for the whole team
+  if (tid == 0) {
+    gu32_p ctr = (gu32_p)(tm.p.ctr + tm.T);
+    __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned want = (unsigned)G * (unsigned)(epoch + 1);
+    unsigned spins = 0;
+    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins > (1u << 24)) {   // seconds: a member is not running (not co-resident); give up, flag it
+        __hip_atomic_store((ECNF_GLOBAL int*)(tm.p.timeout + tm.T), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  // ---- rebuild the aggregates a single workgroup would hold
+  const float* slot0 = base;
+  auto ld16 = [&](int member, int fo) {
+    return *reinterpret_cast<const f32x4*>(slot0 + (size_t)member * tm.p.slot + fo);
+  };
+  for (int idx = tid; idx < N * M4; idx += NTHR) {
+    const int i = idx / M4, c = (idx - i * M4) * 4;
+    const int o0 = first_tile(i) % G, o1 = last_tile(i) % G;
+    f32x4 v = ld16(o0, i * M + c);
+    // atomically accumulated parts (no cross rows): 0 + a + b, whichever member holds each (exact in any order)
+    if (!net.cross && o1 != o0) v += ld16(o1, i * M + c);
+    *reinterpret_cast<f32x4*>(s.macc + i * s.ld_m + c) = v;
+  }
+  if (net.cross)
+    for (int idx = tid; idx < tpm * M4; idx += NTHR) {
+      const int t = idx / M4, c = (idx - t * M4) * 4;
+      *reinterpret_cast<f32x4*>(s.cross + t * s.ld_m + c) = ld16(t % G, off_x + t * M + c);
+    }
+  for (int idx = tid; idx < N * D; idx += NTHR) {
+    const int i = idx / D;
+    const int o0 = first_tile(i) % G, o1 = last_tile(i) % G;
+    float v = slot0[(size_t)o0 * tm.p.slot + off_d + idx];
+    if (o1 != o0) v += slot0[(size_t)o1 * tm.p.slot + off_d + idx];
+    s.dxacc[idx] = v;
+  }
+  __syncthreads();
+}
+
+// ---------------------------------------------------------------------------------------------------
 // one full evaluation.  x_in/tan_in/v_out/tan_out: LDS [MPW][N*D]; t_in: LDS [MPW] (actual time).
 // Must be called by all Geo<NF, NT, P>::NTHR threads of the workgroup (NW waves); returns after a barrier.
 // ---------------------------------------------------------------------------------------------------
-template <int NF, int NT, int L, int D, int P>
+template <int NF, int NT, int L, int D, int P, bool TEAM = false>
 __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const float* x_in, const float* t_in, const float* tan_in,
                           float* v_out, float* tan_out, const int* act = nullptr, int sparse_a = -1,
-                          float* pcache = nullptr, int pmode = 0) {
+                          float* pcache = nullptr, int pmode = 0, const TeamCtx* tm = nullptr,
+                          int* tepoch = nullptr) {
   constexpr int kNW = Geo<NF, NT, P>::NW, kNT = Geo<NF, NT, P>::NTHR;
   constexpr bool kSplitG = Geo<NF, NT, P>::kSplit;
   constexpr bool kSplitN = Geo<NF, NT, P>::kSplitN;   // split node GEMMs (primal split kernels and tangent kernels)
+#ifndef ECNF_NODE_PREFETCH
+#define ECNF_NODE_PREFETCH 0
+#endif
+  // node-GEMM A fragments prefetched across the barrier in front of each node GEMM (node_prefetch): the split primal
+  // kernels (M <= 128; the M = 256 primal kernels need their registers)
+  constexpr bool kPre = ECNF_NODE_PREFETCH && kSplitG && !Geo<NF, NT, P>::kFusedP && NF <= 4;
   // the exact trace's sparse blocks (primal + dual tiles, see the edge loop) in the M <= 128 split tangent kernels;
   // not compiled for the L = 2 shapes (M, D) = (128, 3), (64, 2), where the primal tile's code beside the dual
   // tile's spilled 36 B per lane (tests/test_kernel_resources.py).  The BASELINE shapes (LJ13 128/3/3, ALDP 64/2/3,
@@ -1653,6 +1836,10 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
     int tid = opaque_tid(), lane = tid & 63;
     // the last block's h update (gate, aggregation, phi_h) is dead: the field is x_K - x_c - mean (egnn.py:176-188)
     const bool need_h = k + 1 < net.K;
+    // split primal kernels: each node GEMM's first A fragments are loaded before the barrier in front of it
+    // (node_prefetch; -DECNF_NODE_PREFETCH=0 builds the A/B form without)
+    NodePre pre;
+    if constexpr (kPre) node_prefetch<kNW>(bw.Wn_s, H + T, 0, H, RP, wave, lane, pre);
     // stage this block's chain biases and the w_d / w_g / w_x vectors in LDS (read by every edge tile)
     {
       const float* be = (kSplitG || Geo<NF, NT, P>::kSplitT || Geo<NF, NT, P>::kWideT) ? bw.be_u : bw.be;
@@ -1680,15 +1867,17 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
       __syncthreads();
       STAMP(s, kStNodeDense);
     } else {
-    node_gemm<NT, kNW, kSplitN>(s.hin, s.ld_hin, H + T, nullptr, 0, 0, bw.Wn, bw.Wn_s, bw.ninv, H, bw.bn, H, false, nullptr, 0, s.hb, s.ld_hb, RP,
-                  nvalid, wave, lane);
+    node_gemm<NT, kNW, kSplitN, kPre>(s.hin, s.ld_hin, H + T, nullptr, 0, 0, bw.Wn, bw.Wn_s, bw.ninv, H, bw.bn, H,
+                                      false, nullptr, 0, s.hb, s.ld_hb, RP, nvalid, wave, lane, &pre);
+    if constexpr (kPre && !Geo<NF, NT, P>::kNoP) node_prefetch<kNW>(bw.Wp_s, H, 0, 2 * M, RP, wave, lane, pre);
     __syncthreads();
     STAMP(s, kStNodeDense);
     // per-node halves of phi_e layer 1 (the M = 256 tangent kernels compute layer 1 per edge)
     if constexpr (!Geo<NF, NT, P>::kNoP) {
       constexpr bool kPu = kSplitG || Geo<NF, NT, P>::kL2T;   // log2-domain P
-      node_gemm<NT, kNW, kSplitN>(s.hb, s.ld_hb, H, nullptr, 0, 0, bw.Wp, bw.Wp_s, bw.pinv, 2 * M,
-                                  kPu ? bw.bp_u : bw.bp, 2 * M, false, nullptr, 0, s.P, s.ld_P, RP, nvalid, wave, lane);
+      node_gemm<NT, kNW, kSplitN, kPre>(s.hb, s.ld_hb, H, nullptr, 0, 0, bw.Wp, bw.Wp_s, bw.pinv, 2 * M,
+                                        kPu ? bw.bp_u : bw.bp, 2 * M, false, nullptr, 0, s.P, s.ld_P, RP, nvalid, wave,
+                                        lane, &pre);
       __syncthreads();
     }
     }   // !kFusedP
@@ -1758,7 +1947,9 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
       }
       const int nd = nact * ndt;
       const int nrun = nd + (pload ? 0 : nact * tpm);
-      for (int vt = wave; vt < nrun; vt += kNW) {
+      // team mode (MPW = 1): this member runs tiles t = r, r + G, ... of the molecule (team_exchange)
+      const int tstep = TEAM ? tm->p.G : 1, tfirst = TEAM ? tm->r : 0;
+      for (int vt = tfirst + wave * tstep; vt < nrun; vt += kNW * tstep) {
         if constexpr (kSparseX) {
           if (vt < nd) {
             const int q = vt / ndt;
@@ -1778,7 +1969,14 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
       }
     }
 #endif
+    constexpr bool kHu0 = kSplitG || Geo<NF, NT, P>::kL2T;   // log2-domain messages, scale in phi_h.0
+    if constexpr (kPre)
+      if (need_h) node_prefetch<kNW>(kHu0 ? bw.Wh_s[0] : bw.Wh_sn0, M, H, M, RP, wave, opaque_tid() & 63, pre);
     __syncthreads();
+    if constexpr (TEAM) {   // team mode: rebuild the molecule's aggregates from every member's tiles
+      team_exchange<NT, kNT>(net, s, *tm, *tepoch);
+      ++*tepoch;
+    }
     if constexpr (kSparseX) {
       // first JVP pass of an exact-trace evaluation: cache the sparse block's primal aggregates (see the edge loop)
       if (pcache && pmode == 1 && sparse_a >= 0 && (k == 0 || k + 1 == net.K)) {
@@ -1882,9 +2080,10 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
     float* Q0 = s.P;
     float* Q1 = s.P + (kSplitN ? M + 4 : M + 1);   // 16-B aligned rows for the split node GEMMs
     constexpr bool kHu = kSplitG || Geo<NF, NT, P>::kL2T;   // log2-domain messages, scale in phi_h.0
-    node_gemm<NT, kNW, kSplitN>(s.macc, s.ld_m, M, s.hb, s.ld_hb, H, bw.Wh[0], kHu ? bw.Wh_s[0] : bw.Wh_sn0,
-                                kHu ? bw.hinv[0] : bw.hinv_n0, M, bw.bh[0], M, true, nullptr, 0, Q0, s.ld_P, RP,
-                  nvalid, wave, lane);
+    node_gemm<NT, kNW, kSplitN, kPre>(s.macc, s.ld_m, M, s.hb, s.ld_hb, H, bw.Wh[0], kHu ? bw.Wh_s[0] : bw.Wh_sn0,
+                                      kHu ? bw.hinv[0] : bw.hinv_n0, M, bw.bh[0], M, true, nullptr, 0, Q0, s.ld_P, RP,
+                                      nvalid, wave, lane, &pre);
+    if constexpr (kPre) node_prefetch<kNW>(bw.Wh_s[1], M, 0, L == 1 ? H : M, RP, wave, lane, pre);
     __syncthreads();
     if (!(kSplitG && net.cross)) {   // atomically accumulated aggregates restart from +0
       for (int idx = tid; idx < R * M; idx += kNT) {
@@ -1893,13 +2092,14 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
       }
     }
     for (int l = 1; l < L; ++l) {
-      node_gemm<NT, kNW, kSplitN>(Q0, s.ld_P, M, nullptr, 0, 0, bw.Wh[l], bw.Wh_s[l], bw.hinv[l], M, bw.bh[l], M, true, nullptr, 0, Q1, s.ld_P, RP,
-                    nvalid, wave, lane);
+      node_gemm<NT, kNW, kSplitN, kPre>(Q0, s.ld_P, M, nullptr, 0, 0, bw.Wh[l], bw.Wh_s[l], bw.hinv[l], M, bw.bh[l], M,
+                                        true, nullptr, 0, Q1, s.ld_P, RP, nvalid, wave, lane, &pre);
+      if constexpr (kPre) node_prefetch<kNW>(bw.Wh_s[l + 1], M, 0, l + 1 == L ? H : M, RP, wave, lane, pre);
       __syncthreads();
       float* tq = Q0; Q0 = Q1; Q1 = tq;
     }
-    node_gemm<NT, kNW, kSplitN>(Q0, s.ld_P, M, nullptr, 0, 0, bw.Wh[L], bw.Wh_s[L], bw.hinv[L], H, bw.bh[L], H, false, s.hb, s.ld_hb, s.hin, s.ld_hin, RP,
-                  nvalid, wave, lane);
+    node_gemm<NT, kNW, kSplitN, kPre>(Q0, s.ld_P, M, nullptr, 0, 0, bw.Wh[L], bw.Wh_s[L], bw.hinv[L], H, bw.bh[L], H,
+                                      false, s.hb, s.ld_hb, s.hin, s.ld_hin, RP, nvalid, wave, lane, &pre);
     __syncthreads();
     STAMP(s, kStPhiH);
   }

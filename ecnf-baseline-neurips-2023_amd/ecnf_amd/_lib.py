@@ -27,6 +27,7 @@ EXPORTED_SYMBOLS = (
     "ecnf_set_precision", "ecnf_get_precision", "ecnf_trainer_create", "ecnf_trainer_destroy", "ecnf_fm_loss_grad",
     "ecnf_adam_update", "ecnf_update_params", "ecnf_integrate_workspace_size", "ecnf_integrate_ws",
     "ecnf_reserve_workspace", "ecnf_set_exact_form", "ecnf_struct_layout", "ecnf_trainer_set_reduction_arena",
+    "ecnf_set_team", "ecnf_team_workgroups",
 )
 
 TARGET_LJ, TARGET_DW = 0, 1
@@ -154,9 +155,13 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
         "ecnf_integrate_ws": ([P, ctypes.POINTER(EcnfSolveOpts), P, P, P, P, P, P, P, I32, P, SZ, P], ctypes.c_int),
         "ecnf_reserve_workspace": ([P, SZ], ctypes.c_int),
         "ecnf_set_exact_form": ([P, I32], ctypes.c_int),
+        "ecnf_set_team": ([P, I32], ctypes.c_int),
+        "ecnf_team_workgroups": ([P, I32, I32, ctypes.POINTER(I32)], ctypes.c_int),
         "ecnf_struct_layout": ([I32, ctypes.POINTER(SZ), I32], ctypes.c_int),
     }
     for name, (argtypes, restype) in sig.items():
+        if path != LIB_PATH and not hasattr(lib, name):
+            continue   # an older A/B timing build (ECNF_LIB, tools/build_timing.sh) may predate an entry point
         fn = getattr(lib, name)
         fn.argtypes = argtypes
         fn.restype = restype

@@ -265,6 +265,9 @@ class EcnfHandle:
                 n_nf = int((st == _lib.ECNF_E_NONFINITE).sum())
                 if n_nf:
                     raise RuntimeError(f"{n_nf} molecule(s) ended with a non-finite state")
+                n_hip = int((st == _lib.ECNF_E_HIP).sum())
+                if n_hip:
+                    raise RuntimeError(f"{n_hip} molecule(s) failed on the device (a team exchange timed out)")
         return y1, dl, nfe, status
 
     def _integrate(self, y0, f, e, t0, t1, opts: SolveOptions, divergence: int):
@@ -291,6 +294,16 @@ class EcnfHandle:
         forms = {"default": _lib.EXACT_FORM_DEFAULT, "all_dual": _lib.EXACT_FORM_ALL_DUAL,
                  "sparse": _lib.EXACT_FORM_SPARSE}
         _lib.check(self.lib.ecnf_set_exact_form(self._h, forms[form]))
+
+    def set_team(self, mode: int = 0) -> None:
+        """Team (latency) mode of the primal solves (ecnf_set_team): 0 auto, 1 off, G >= 2 workgroups per molecule."""
+        _lib.check(self.lib.ecnf_set_team(self._h, int(mode)))
+
+    def team_workgroups(self, batch: int, with_tangent: bool = False) -> int:
+        """Workgroups per molecule a solve of `batch` molecules would use (1: the batch path)."""
+        g = ctypes.c_int32()
+        _lib.check(self.lib.ecnf_team_workgroups(self._h, int(with_tangent), int(batch), ctypes.byref(g)))
+        return g.value
 
     def base_sample(self, z) -> torch.Tensor:
         z = self._f32(z, (self.cfg.event_dim,), "z")

@@ -148,6 +148,17 @@ int ecnf_reserve_workspace(ecnf_handle* h, size_t bytes);
 enum ecnf_exact_form { ECNF_EXACT_FORM_DEFAULT = 0, ECNF_EXACT_FORM_ALL_DUAL = 1, ECNF_EXACT_FORM_SPARSE = 2 };
 int ecnf_set_exact_form(ecnf_handle* h, int32_t form);
 
+/* Team (latency) mode of the primal solves (DIV_NONE: sample_cnf), for batches far below the CU count -- the
+ * reference's one-molecule-per-call sampling timer (examples/load_checkpoint_measure_sampling_time.py:101-119):
+ * G workgroups integrate one molecule together, its edge tiles dealt over them, the edge aggregates exchanged through
+ * global memory after every block's edge phase (a cooperative launch of batch x G workgroups).  Results are bitwise
+ * those of the batch path.  mode: 0 auto (G = ceil(edge tiles / waves) when M = 256, batch x G <= CUs and
+ * batch <= 32), 1 off, G >= 2 forced (capped by the handle's buffers).  ecnf_team_workgroups reports the G a solve of
+ * `batch` molecules would use (1: the batch path).  A team whose exchange times out (a member not co-resident)
+ * reports status ECNF_E_HIP for its molecule. */
+int ecnf_set_team(ecnf_handle* h, int32_t mode);
+int ecnf_team_workgroups(ecnf_handle* h, int32_t with_tangent, int32_t batch, int32_t* G);
+
 /* x0 = base_scale * (z - mean_nodes(z)) for a standard-normal draw z [batch, N*D]. */
 int ecnf_base_sample(ecnf_handle* h, const float* z, float* x0, int32_t batch, void* stream);
 

@@ -151,7 +151,7 @@ def test_base_distribution():
     x = h.base_sample(g(z))
     assert rel_err(x, O.base_sample(z, oc, np.float64)) <= 1e-6
     lp = h.base_log_prob(g(x0))
-    assert np.abs(lp.cpu().numpy() - O.base_log_prob(x0, oc)).max() <= 1e-3
+    fp32_class("aldp base log_prob", lp, O.base_log_prob(x0, oc, np.float64), O.base_log_prob(x0, oc, np.float32))
 
 
 @pytest.mark.parametrize("name", ["lj13", "dw4"])

@@ -169,20 +169,29 @@ def test_wide_nonfinite_divergence_reruns_on_strict_fp32():
 
 def test_wide_fp32_adaptive_sample_and_log_prob():
     """sample_and_log_prob_cnf with the reference's default adaptive solve (Dopri5 + PID, rtol = atol = 1e-5) through
-    the strict-fp32 M = 256 tangent kernels: the PID step sequence is chaotic in fp32, so (as test_gpu_parity's adaptive
-    cases) the end point must land within the spread of the oracle's fp32 adaptive solves; the step counts of two
-    molecules are as chaotic (a first run: 63 / 159 vs the fp64 oracle's 57 / 111), so NFE only within 50 %."""
+    the strict-fp32 M = 256 tangent kernels, held to the envelope of test_gpu_eval_modes.py: the fp32 oracle's adaptive
+    solves of x0 and of 5 copies perturbed by 1e-7 relative against an fp64 truth (Dopri5, fixed dt = 0.005).
+
+    Round 3 compared the kernel's NFE (63 / 159) with the fp64 ADAPTIVE oracle's (57 / 111) and widened the bound to
+    50 %.  The fp32 oracle's own NFE for these molecules is 57 ... 69 and 117 ... 267 over x0 and the perturbed copies
+    (x0 alone: 63 / 267): the second molecule's step sequence is chaotic in fp32, the controller is not different.  So
+    the bound is the 30 % one against that fp32 envelope: each molecule's NFE within [0.7 min, 1.3 max]."""
+    from test_gpu_eval_modes import envelope, nfe_envelope
+    from test_gpu_parity import _perturbed
     cfg = WIDE_TINY
     oc, params, h, z, x0, feat = setup_prec(cfg, 2, "fp32")
-    x1, dl, nfe, st = h.integrate(g(x0), g(feat, torch.int32), 0.0, 1.0, SolveOptions("dopri5", None),
+    xd = h.base_sample(g(z))
+    x1, dl, nfe, st = h.integrate(xd, g(feat, torch.int32), 0.0, 1.0, SolveOptions("dopri5", None),
                                   divergence=_lib.DIV_HUTCHINSON, eps=g(z))
     assert int(st.abs().sum()) == 0
-    x64, lq64, nfe64 = O.sample_and_log_prob(params, oc, x0, feat, eps=z, approx=True, solver="dopri5", dt0=None,
-                                             dtype=np.float64)
-    x32, lq32, _ = O.sample_and_log_prob(params, oc, x0, feat, eps=z, approx=True, solver="dopri5", dt0=None,
-                                         dtype=np.float32)
-    spread = max(float(np.abs(x32 - x64).max()), 1e-6)
-    assert float(np.abs(x1.cpu().numpy() - x64).max()) <= 2 * spread + 2e-4
-    lq = (h.base_log_prob(g(x0)) - dl).cpu().numpy()
-    assert float(np.abs(lq - lq64).max()) <= 2 * max(float(np.abs(lq32 - lq64).max()), 1e-6) + 2e-3
-    assert abs(float(nfe.float().mean()) - float(np.mean(nfe64))) <= 0.5 * float(np.mean(nfe64))
+    xf, lqf, _ = O.sample_and_log_prob(params, oc, x0, feat, eps=z, approx=True, solver="dopri5", dt0=0.005,
+                                       dtype=np.float64)
+    xs, lqs, nfes = [], [], []
+    for k in range(6):
+        x32, lq32, n32 = O.sample_and_log_prob(params, oc, _perturbed(x0, k), feat, eps=z, approx=True,
+                                               solver="dopri5", dt0=None, dtype=np.float32)
+        xs.append(x32), lqs.append(lq32), nfes.append(n32)
+    nfe_envelope("wide fp32 adaptive", nfe, np.stack(nfes))
+    envelope("wide fp32 adaptive x1", x1, xf, np.stack(xs), 2e-4)
+    lq = h.base_log_prob(xd) - dl
+    envelope("wide fp32 adaptive log_q", lq, lqf, np.stack(lqs), 1e-4 * max(1.0, float(np.abs(lqf).max())))
