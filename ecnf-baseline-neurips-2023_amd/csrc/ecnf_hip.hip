@@ -618,6 +618,19 @@ hipError_t dispatch_integrate(const ecnf_handle* h, int NT, const SolveP& sp_in,
   } else {
     sp.team = TeamP{};
     net = net_for_batch(h, ix, B, &lds, sp.adaptive != 0);
+    // halves mode (integrate_kernel HALF): a workgroup of m = 2 m' molecules runs as two independent halves of m'
+    // (own LDS, solver and barriers), so one half's node phases overlap the other's edge chains
+    const int m = net.MPW;
+    if (ECNF_HALVES && NT == 0 && split_primal(h->cfg, 0, P) && primal_waves(h->cfg) == 8 && m % 2 == 0) {
+      const int mh = m / 2, RP = 32 * ((mh * h->cfg.n_nodes + 31) / 32);
+      const size_t lh = lds_bytes(h->cfg, 0, P, mh, RP);
+      if (2 * lh <= 160 * 1024) {
+        set_mpw(net, h->cfg, 0, P, mh, RP);
+        net.lds_floats = (int)(lh / 4);
+        lds = lh;
+        sp.halves = 1;
+      }
+    }
   }
 #define ECNF_CALL(m, l, d, nt, p) \
   launch_integrate<m / 32, nt, l, d, p>(net, lds, sp, y0, feat, eps, y1, dlogp, nfe, status, B, stream)
@@ -1281,6 +1294,7 @@ int integrate_impl(ecnf_handle* h, const ecnf_solve_opts* o, const float* y0, co
   sp.pcache = nullptr;
   sp.pcache_slots = 0;
   sp.team = TeamP{};   // dispatch_integrate sets it (team_size)
+  sp.halves = 0;       // ... and this (halves mode)
   const size_t need = sp.sparse1 ? pcache_floats(h, batch) : 0;
   // the arena pointer and size are read under arena_mu, and the lock is held through the dispatch that uses them:
   // an ecnf_reserve_workspace on another thread cannot free the arena between the read and the launch

@@ -52,6 +52,9 @@ struct SolveP {
   // team (latency) mode of the primal kernels (egnn_eval.hpp team_exchange): team.G > 1 workgroups per molecule,
   // MPW = 1, grid = batch x G (a cooperative launch: every member co-resident)
   TeamP team;
+  // halves mode (integrate_kernel HALF): 1 = launch 512-thread workgroups of two independent 256-thread halves with
+  // net.MPW molecules and net.lds_floats floats of LDS each (the host sets it for halves_shape kernels)
+  int halves;
 };
 
 // solver state in LDS, after the eval region
@@ -59,10 +62,14 @@ struct SolverLds {
   float *ys, *vout, *tin, *tout, *y, *eps, *kx;   // [MPW][ND] each, kx [7][MPW][ND]
   float *ts, *divv, *lp, *kl, *tau, *tnext, *dt, *h, *l1, *h0;   // [MPW] (kl: [7][MPW])
   int *active, *atmin, *nfe, *steps, *status, *keep, *any;
+  // the phase machine's uniform control state (integrate_kernel): [0] Euler tau, [1] Euler next tau (float bits),
+  // [2] Euler steps, [3] phase, [4] stage.  Read from LDS on both sides of every evaluation instead of being held in
+  // registers across it (held, they spilled)
+  int* ctl;
 };
 
 __host__ __device__ inline int solver_lds_floats(int MPW, int ND) {
-  return 13 * align4(MPW * ND) + 16 * align4(MPW) + 8 * align4(MPW) + 4;
+  return 13 * align4(MPW * ND) + 16 * align4(MPW) + 8 * align4(MPW) + 4 + 8;
 }
 
 __device__ inline SolverLds carve_solver(float* p, int MPW, int ND) {
@@ -75,7 +82,8 @@ __device__ inline SolverLds carve_solver(float* p, int MPW, int ND) {
   st.l1 = p; p += b;  st.h0 = p; p += b;
   int* q = reinterpret_cast<int*>(p);
   st.active = q; q += b; st.atmin = q; q += b; st.nfe = q; q += b; st.steps = q; q += b;
-  st.status = q; q += b; st.keep = q; q += b; st.any = q;
+  st.status = q; q += b; st.keep = q; q += b; st.any = q; q += 4;
+  st.ctl = q;
   return st;
 }
 
@@ -98,11 +106,13 @@ __device__ inline bool check_features(const Net& net, int* f) {
 
 // one evaluation of the joint field g(tau, y) = dir * f(dir * tau, y) at (st.ts, st.ys) for every molecule
 // of the workgroup; writes kx_out [MPW][ND] and kl_out [MPW].  Exactly one egnn_eval call site (it is inlined).
-template <int NF, int NT, int L, int D, int P, bool TEAM>
+template <int NF, int NT, int L, int D, int P, bool TEAM, bool HALF>
 __device__ __forceinline__ void joint_field(const Net& net, const Lds& s, const SolverLds& st, const SolveP& sp,
                                             float* kx_out, float* kl_out, const TeamCtx* tm, int* tepoch) {
-  constexpr int kThreads = Geo<NF, NT, P>::NTHR;
-  const int tid = opaque_tid(), MPW = net.MPW, ND = net.ND;
+  constexpr int kThreads = HALF ? 256 : Geo<NF, NT, P>::NTHR;
+  // per-thread indices are re-derived (opaque_tid) on each side of the evaluation: kept live across it, they spill
+  const int MPW = opaque_u(net.MPW), ND = opaque_u(net.ND);
+  int tid = vtid<HALF>();
   // NT == 0: one primal eval; Hutchinson: one JVP along eps; exact: the trace of J from ND - D JVPs along e_k,
   // k >= D.  The field only sees relative positions and subtracts the input mean (egnn.py:176-188), so
   // v(x + s 1) = v(x) - s exactly, i.e. J T_c = -T_c for the translations T_c = sum_a e_(a,c).  In the basis
@@ -114,13 +124,14 @@ __device__ __forceinline__ void joint_field(const Net& net, const Lds& s, const 
   if (tid < MPW) st.divv[tid] = exact ? -(float)D : 0.f;
   for (int k0 = 0; k0 < nrep; ++k0) {
     const int k = exact ? k0 + D : k0;
+    tid = vtid<HALF>();
     if constexpr (NT) {
       if (sp.div == ECNF_DIV_HUTCHINSON) {
         for (int i = tid; i < MPW * ND; i += kThreads) st.tin[i] = st.eps[i];
       } else {
         for (int i = tid; i < MPW * ND; i += kThreads) st.tin[i] = ((i % ND) == k) ? 1.0f : 0.0f;
       }
-      __syncthreads();
+      wg_sync<HALF>();
     }
     // exact: the unit tangent e_k sits on atom k / D, so block 1 (whose node features carry no tangent) has nonzero
     // edge tangents only on the 2(N - 1) edges at that atom
@@ -129,8 +140,9 @@ __device__ __forceinline__ void joint_field(const Net& net, const Lds& s, const 
                     ? sp.pcache + (size_t)blockIdx.x * MPW * (net.N * (NF * 32) + 2 * net.N * D)
                     : nullptr;
     ECNF_DCHECK(!pc || (int)(blockIdx.x + 1) * MPW <= sp.pcache_slots, 6);
-    egnn_eval<NF, NT, L, D, P, TEAM>(net, s, st.ys, st.ts, st.tin, st.vout, st.tout, st.active, sparse ? k / D : -1,
+    egnn_eval<NF, NT, L, D, P, TEAM, HALF>(net, s, st.ys, st.ts, st.tin, st.vout, st.tout, st.active, sparse ? k / D : -1,
                                      pc, k0 == 0 ? 1 : 2, tm, tepoch);
+    tid = vtid<HALF>();
     if constexpr (NT) {
       if (tid < MPW) {
         if (sp.div == ECNF_DIV_HUTCHINSON) {
@@ -143,12 +155,13 @@ __device__ __forceinline__ void joint_field(const Net& net, const Lds& s, const 
       }
     }
   }
+  tid = vtid<HALF>();
   for (int i = tid; i < MPW * ND; i += kThreads) kx_out[i] = sp.dirf * st.vout[i];
   if (tid < MPW) {
     kl_out[tid] = sp.dirf * st.divv[tid];
     if (st.active[tid]) st.nfe[tid] += 1;
   }
-  __syncthreads();
+  wg_sync<HALF>();
 }
 
 // diffrax rms_norm over the leaves of one molecule's state: (x, logp) when the divergence is tracked
@@ -161,15 +174,23 @@ enum Phase { kEuler = 0, kInit0 = 1, kInit1 = 2, kFsal = 3, kStage = 4 };
 
 // The whole solve as a phase machine around ONE field evaluation per loop trip.  TEAM: the team (latency) mode
 // instantiation (egnn_eval.hpp team_exchange; launched only with sp.team.G > 1, compiled for team_shape)
-template <int NF, int NT, int L, int D, int P, bool TEAM = false>
-__global__ __launch_bounds__((Geo<NF, NT, P>::NTHR)) __attribute__((amdgpu_waves_per_eu(Geo<NF, NT, P>::WPE))) void integrate_kernel(Net net, SolveP sp, const float* __restrict__ y0,
+template <int NF, int NT, int L, int D, int P, bool TEAM = false, bool HALF = false>
+__global__ __launch_bounds__((HALF ? 512 : Geo<NF, NT, P>::NTHR)) __attribute__((amdgpu_waves_per_eu(Geo<NF, NT, P>::WPE))) void integrate_kernel(Net net, SolveP sp, const float* __restrict__ y0,
                                                                   const int32_t* __restrict__ feat,
                                                                   const float* __restrict__ eps, float* y1,
                                                                   float* dlogp, int32_t* nfe_out,
                                                                   int32_t* status_out, int B) {
-  constexpr int kThreads = Geo<NF, NT, P>::NTHR;
-  extern __shared__ float smem[];
-  const int tid = threadIdx.x, MPW = net.MPW, ND = net.ND, N = net.N;
+  // HALF (halves mode, egnn_eval.hpp wg_sync): two independent 256-thread halves, half h = threadIdx.x / 256 with
+  // its own net.lds_floats of LDS and molecules [(2 blockIdx + h) MPW, +MPW)
+  constexpr int kThreads = HALF ? 256 : Geo<NF, NT, P>::NTHR;
+  extern __shared__ float smem_all[];
+  const int half = HALF ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 8)) : 0;
+  if constexpr (HALF) {
+    if (threadIdx.x < 4) half_bar_words()[threadIdx.x] = 0;
+    __syncthreads();   // the only workgroup barrier of a halves kernel: both halves start together
+  }
+  float* smem = smem_all + (HALF ? half * net.lds_floats : 0);
+  const int tid = HALF ? (int)(threadIdx.x & 255) : (int)threadIdx.x, MPW = net.MPW, ND = net.ND, N = net.N;
   const Lds s = carve_lds<NT, Geo<NF, NT, P>::kSplitN, Geo<NF, NT, P>::kNoP>(net, smem);
   const SolverLds st = carve_solver(s.tail, MPW, ND);
   // team mode: workgroup blockIdx = T G + r is member r of molecule T's team (MPW = 1); only member 0 writes outputs
@@ -181,16 +202,17 @@ __global__ __launch_bounds__((Geo<NF, NT, P>::NTHR)) __attribute__((amdgpu_waves
   const TeamCtx* tm = team ? &team_ctx : nullptr;
   int tepoch = 0;
   const bool writer_wg = team_ctx.r == 0;
-  const int mol0 = team ? team_ctx.T : blockIdx.x * MPW;
+  const int mol0 = team ? team_ctx.T : HALF ? (2 * (int)blockIdx.x + half) * MPW : (int)blockIdx.x * MPW;
   const int nmol = min(MPW, B - mol0);
-  const int a = align4(MPW * ND), b = align4(MPW);
+  if constexpr (HALF)
+    if (nmol <= 0) return;   // the second half of the last workgroup has no molecules (it never syncs again)
   ECNF_DCHECK((int)(s.tail - smem) + solver_lds_floats(MPW, ND) <= net.lds_floats, 0);
   ECNF_DCHECK(nmol >= 1 && nmol <= MPW, 5);
   const bool track = sp.div != ECNF_DIV_NONE;
 
   // zero the eval scratch (aggregates must start at +0; padding rows stay finite)
   for (int i = tid; i < (int)(s.tail - smem); i += kThreads) smem[i] = 0.f;
-  __syncthreads();
+  wg_sync<HALF>();
   for (int i = tid; i < MPW * ND; i += kThreads) {
     const int m = i / ND;
     st.y[i] = m < nmol ? y0[(size_t)mol0 * ND + i] : 0.f;
@@ -208,18 +230,20 @@ __global__ __launch_bounds__((Geo<NF, NT, P>::NTHR)) __attribute__((amdgpu_waves
     st.dt[tid] = sp.dt0;
     st.tnext[tid] = clip_end(fminf(sp.tau0 + sp.dt0, sp.tau1), sp.tau1);
   }
-  __syncthreads();
+  if (tid == 0) {
+    // Euler: ConstantStepSize, all molecules share the (uniform) time grid
+    st.ctl[0] = __builtin_bit_cast(int, sp.tau0);
+    st.ctl[1] = __builtin_bit_cast(int, clip_end(sp.tau0 + sp.dt0, sp.tau1));
+    st.ctl[2] = 0;
+    st.ctl[3] = sp.solver == ECNF_SOLVER_EULER ? kEuler : (sp.adaptive ? kInit0 : kFsal);
+    st.ctl[4] = 1;
+  }
+  wg_sync<HALF>();
   // device-side input check (no host sync on the call path): a molecule with an embedding id outside
   // [0, n_features) reports ECNF_E_INVALID (nn.Embed would index out of range) and is solved with id 0
   if (tid < nmol && !check_features(net, s.feat + tid * N)) st.status[tid] = ECNF_E_INVALID;
-  __syncthreads();
+  wg_sync<HALF>();
 
-  // Euler: ConstantStepSize, all molecules share the (uniform, register-held) time grid
-  // (wave-uniform values pinned to SGPRs with readfirstlane: as VGPRs they are live across every eval and spill)
-  float e_tau = sp.tau0, e_tn = uniform_f(clip_end(sp.tau0 + sp.dt0, sp.tau1)), e_h = 0.f;
-  int e_steps = 0;
-  int phase = sp.solver == ECNF_SOLVER_EULER ? kEuler : (sp.adaptive ? kInit0 : kFsal);
-  int stage = 1;
 
 #ifdef ECNF_STAMPS
   if (tid == 0) {
@@ -229,7 +253,14 @@ __global__ __launch_bounds__((Geo<NF, NT, P>::NTHR)) __attribute__((amdgpu_waves
   }
 #endif
   while (true) {
-    const int tid = opaque_tid();   // shadows the kernel-level tid: nothing per-thread stays live across an eval
+    const int tid = vtid<HALF>();   // shadows the kernel-level tid: nothing per-thread stays live across an eval
+    const int MPW = opaque_u(net.MPW), ND = opaque_u(net.ND);   // (likewise the sizes, the solver-state pointers)
+    const SolverLds st = carve_solver(opaque_smem(s.tail), MPW, ND);
+    const int a = align4(MPW * ND), b = align4(MPW);
+    // the control state, wave-uniform (SGPRs)
+    float e_tau = uniform_f(__builtin_bit_cast(float, st.ctl[0])), e_tn = uniform_f(__builtin_bit_cast(float, st.ctl[1]));
+    int e_steps = __builtin_amdgcn_readfirstlane(st.ctl[2]);
+    int phase = __builtin_amdgcn_readfirstlane(st.ctl[3]), stage = __builtin_amdgcn_readfirstlane(st.ctl[4]);
     STAMP(s, kStSolver);
     // ------------------------------------------------ inputs of this evaluation
     float* kx_out;
@@ -240,7 +271,6 @@ __global__ __launch_bounds__((Geo<NF, NT, P>::NTHR)) __attribute__((amdgpu_waves
         if (tid < nmol) st.status[tid] = ECNF_E_MAX_STEPS;
         break;
       }
-      e_h = uniform_f(e_tn - e_tau);
       for (int i = tid; i < MPW * ND; i += kThreads) st.ys[i] = st.y[i];
       if (tid < MPW) st.ts[tid] = sp.dirf * e_tau;
       kx_out = st.kx; kl_out = st.kl;
@@ -260,7 +290,7 @@ __global__ __launch_bounds__((Geo<NF, NT, P>::NTHR)) __attribute__((amdgpu_waves
           *st.any = any;
         }
         if (tid < MPW) st.h[tid] = st.tnext[tid] - st.tau[tid];
-        __syncthreads();
+        wg_sync<HALF>();
         if (*st.any == 0) break;
       }
       for (int i = tid; i < MPW * ND; i += kThreads) {
@@ -271,11 +301,24 @@ __global__ __launch_bounds__((Geo<NF, NT, P>::NTHR)) __attribute__((amdgpu_waves
       if (tid < MPW) st.ts[tid] = sp.dirf * (st.tau[tid] + kC[stage] * st.h[tid]);
       kx_out = st.kx + stage * a; kl_out = st.kl + stage * b;
     }
-    __syncthreads();
+    wg_sync<HALF>();
 
-    joint_field<NF, NT, L, D, P, TEAM>(net, s, st, sp, kx_out, kl_out, tm, &tepoch);
+    joint_field<NF, NT, L, D, P, TEAM, HALF>(net, s, st, sp, kx_out, kl_out, tm, &tepoch);
 
     // ------------------------------------------------ consume it
+    {
+    // per-thread indices, solver pointers and the control state re-derived after the evaluation (nothing of the
+    // trip's first half stays live across it)
+    const int tid = vtid<HALF>();
+    const int MPW = opaque_u(net.MPW), ND = opaque_u(net.ND);
+    const SolverLds st = carve_solver(opaque_smem(s.tail), MPW, ND);
+    const int a = align4(MPW * ND), b = align4(MPW);
+    e_tau = uniform_f(__builtin_bit_cast(float, st.ctl[0]));
+    e_tn = uniform_f(__builtin_bit_cast(float, st.ctl[1]));
+    phase = __builtin_amdgcn_readfirstlane(st.ctl[3]);
+    e_steps = __builtin_amdgcn_readfirstlane(st.ctl[2]) + (phase == kEuler ? 1 : 0);   // (this trip's Euler step)
+    stage = __builtin_amdgcn_readfirstlane(st.ctl[4]);
+    const float e_h = uniform_f(e_tn - e_tau);
     if (phase == kEuler) {
       for (int i = tid; i < MPW * ND; i += kThreads) st.y[i] = st.y[i] + e_h * st.kx[i];
       if (tid < MPW) st.lp[tid] = st.lp[tid] + e_h * st.kl[tid];
@@ -364,7 +407,7 @@ __global__ __launch_bounds__((Geo<NF, NT, P>::NTHR)) __attribute__((amdgpu_waves
         st.dt[m] = new_dt;
         st.h0[m] = (float)new_atmin;
       }
-      __syncthreads();
+      wg_sync<HALF>();
       for (int i = tid; i < MPW * ND; i += kThreads) {
         const int m = i / ND;
         if (st.keep[m]) {
@@ -394,11 +437,19 @@ __global__ __launch_bounds__((Geo<NF, NT, P>::NTHR)) __attribute__((amdgpu_waves
       }
       stage = 1;
     }
-    __syncthreads();
+    if (tid == 0) {   // the control state of the next trip (read by every thread after the barrier)
+      st.ctl[0] = __builtin_bit_cast(int, e_tau);
+      st.ctl[1] = __builtin_bit_cast(int, e_tn);
+      st.ctl[2] = e_steps;
+      st.ctl[3] = phase;
+      st.ctl[4] = stage;
+    }
+    wg_sync<HALF>();
+    }   // consume
   }
-  __syncthreads();
+  wg_sync<HALF>();
 #ifdef ECNF_STAMPS
-  if (tid == 0) {
+  if (threadIdx.x == 0) {
     STAMP(s, kStSolver);
     s.stamps[29] = __builtin_amdgcn_s_memrealtime() - s.stamps[30];
     for (int i = 0; i < kStCount; ++i) atomicAdd(&g_stamps[i], s.stamps[i]);
@@ -407,7 +458,11 @@ __global__ __launch_bounds__((Geo<NF, NT, P>::NTHR)) __attribute__((amdgpu_waves
   }
 #endif
   // failure detection: a final state that is not finite (activations beyond the fp16 range of the split GEMMs, an
-  // overflowing field) is reported per molecule instead of passing as ECNF_OK
+  // overflowing field) is reported per molecule instead of passing as ECNF_OK.  (tid and the solver-state pointers
+  // re-derived here: kept from the kernel's start, they would stay live across the whole solve and spill.)
+  {
+  const int tid = vtid<HALF>();
+  const SolverLds st = carve_solver(opaque_smem(s.tail), MPW, ND);
   if (tid < nmol && st.status[tid] == ECNF_OK) {
     bool fin = isfinite(st.lp[tid]);
     for (int c = 0; c < ND; ++c) fin = fin && isfinite(st.y[tid * ND + c]);
@@ -418,7 +473,7 @@ __global__ __launch_bounds__((Geo<NF, NT, P>::NTHR)) __attribute__((amdgpu_waves
     if (tid == 0 && __hip_atomic_load((ECNF_GLOBAL int*)(sp.team.timeout + team_ctx.T), __ATOMIC_RELAXED,
                                       __HIP_MEMORY_SCOPE_AGENT))
       st.status[0] = ECNF_E_HIP;
-    __syncthreads();
+    wg_sync<HALF>();
     if (!writer_wg) return;
   }
   for (int i = tid; i < nmol * ND; i += kThreads) y1[(size_t)mol0 * ND + i] = st.y[i];
@@ -426,6 +481,7 @@ __global__ __launch_bounds__((Geo<NF, NT, P>::NTHR)) __attribute__((amdgpu_waves
     if (dlogp) dlogp[mol0 + tid] = st.lp[tid];
     if (nfe_out) nfe_out[mol0 + tid] = st.nfe[tid];
     if (status_out) status_out[mol0 + tid] = st.status[tid];
+  }
   }
 }
 
@@ -476,6 +532,16 @@ __global__ __launch_bounds__((Geo<NF, NT, P>::NTHR)) __attribute__((amdgpu_waves
   }
 }
 
+// halves-mode kernels (integrate_kernel HALF): the 8-wave split primal kernels (M <= 128); -DECNF_HALVES=0 builds
+// without them (A/B)
+#ifndef ECNF_HALVES
+#define ECNF_HALVES 1
+#endif
+template <int NF, int NT, int P>
+constexpr bool halves_shape() {
+  return ECNF_HALVES && NT == 0 && Geo<NF, NT, P>::kSplit && NF <= 4 && Geo<NF, NT, P>::NW == 8;
+}
+
 // shapes with a team-mode kernel (ecnf_hip.hip team_size): the split primal kernels of the BASELINE networks
 // (QM9 M = 256, LJ13 M = 128, ALDP M = 64)
 constexpr bool team_shape(int M, int NT, int L, int D, int P) {
@@ -506,6 +572,17 @@ hipError_t launch_integrate(const Net& net, size_t lds, const SolveP& sp, const 
     }
   }
   if (sp.team.G > 1) return hipErrorInvalidValue;   // no team kernel for this shape (team_size never asks for one)
+  if constexpr (halves_shape<NF, NT, P>()) {
+    if (sp.halves) {
+      auto kh = integrate_kernel<NF, NT, L, D, P, false, true>;
+      hipError_t e = hipFuncSetAttribute((const void*)kh, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(2 * lds));
+      if (e != hipSuccess) return e;
+      const int grid = (B + 2 * net.MPW - 1) / (2 * net.MPW);
+      hipLaunchKernelGGL(kh, dim3(grid), dim3(512), 2 * lds, stream, net, sp, y0, feat, eps, y1, dlogp, nfe, status, B);
+      return hipGetLastError();
+    }
+  }
+  if (sp.halves) return hipErrorInvalidValue;
   auto k = integrate_kernel<NF, NT, L, D, P>;
   hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;

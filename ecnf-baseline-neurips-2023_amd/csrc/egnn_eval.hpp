@@ -203,7 +203,7 @@ struct Net {
 // ---------------------------------------------------------------------------------------------------
 enum StampSlot {
   kStPrologue = 0, kStNodeDense, kStPGemm, kStEdge, kStNodeUpd, kStPhiH, kStEpilogue, kStSolver,
-  kStEdgeChainE, kStEdgeTail, kStEdgeLayer1, kStEdgeAgg, kStEdgePhiXIn, kStEdgePhiX, kStCount
+  kStEdgeChainE, kStEdgeTail, kStEdgeLayer1, kStEdgeAgg, kStEdgePhiXIn, kStEdgePhiX, kStTeam, kStCount
 };
 #ifdef ECNF_STAMPS
 __device__ unsigned long long g_stamps[32];
@@ -360,6 +360,62 @@ __device__ __forceinline__ int opaque_tid() {
   int t = threadIdx.x;
   asm volatile("" : "+v"(t));
   return t;
+}
+
+// a wave-uniform int through an empty asm: sizes used as divisors in per-evaluation loops (i / ND, i % ND) are seen
+// afresh at each use site, so the compiler does not hoist their division constants out of the solver loop and keep
+// them live (in VGPRs, which then spill) across every evaluation
+__device__ __forceinline__ int opaque_u(int v) {
+  v = __builtin_amdgcn_readfirstlane(v);
+  asm volatile("" : "+s"(v));
+  return v;
+}
+
+// Halves mode (egnn_eval / integrate_kernel HALF): a 512-thread workgroup runs as two independent 256-thread halves
+// (waves 0-3 and 4-7; waves w and w + 4 share a SIMD), each with its own molecules, LDS region and solver, and
+// synchronised by its own LDS barrier instead of s_barrier, so one half's latency-bound node phases overlap the other
+// half's edge chains on the same SIMDs.  vtid: the thread index within the (half) workgroup.
+template <bool HALF>
+__device__ __forceinline__ int vtid() {
+  return HALF ? (opaque_tid() & 255) : opaque_tid();
+}
+
+// the barrier of a half: an LDS arrival counter and generation word per half (sense by generation); the LDS writes
+// of each wave are complete (lgkmcnt(0)) before it arrives.  Never mixed with s_barrier after the kernel's start.
+__device__ __forceinline__ int* half_bar_words() {
+  __shared__ int bar[2][2];   // [half][arrivals, generation]; zeroed at the kernel's start (integrate_kernel)
+  return &bar[0][0];
+}
+__device__ __forceinline__ void half_barrier() {
+  int* bar = half_bar_words() + 2 * __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 8));
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  const int gen = __builtin_amdgcn_readfirstlane(__hip_atomic_load(bar + 1, __ATOMIC_RELAXED,
+                                                                   __HIP_MEMORY_SCOPE_WORKGROUP));
+  int arrived = 0;
+  if ((threadIdx.x & 63) == 0)
+    arrived = __hip_atomic_fetch_add(bar, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  arrived = __builtin_amdgcn_readfirstlane(arrived);
+  if (arrived == 3) {   // the last of the half's 4 waves: reset the count, then release the generation
+    if ((threadIdx.x & 63) == 0) {
+      __hip_atomic_store(bar, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      __hip_atomic_store(bar + 1, gen + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+  } else {
+    // bounded (seconds): a wave that never arrives would be a bug; the kernel then finishes with wrong results
+    // instead of hanging the device
+    for (unsigned spins = 0; __builtin_amdgcn_readfirstlane(__hip_atomic_load(bar + 1, __ATOMIC_RELAXED,
+                                                                              __HIP_MEMORY_SCOPE_WORKGROUP)) == gen &&
+                             spins < (1u << 26);
+         ++spins)
+      __builtin_amdgcn_s_sleep(1);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
+template <bool HALF>
+__device__ __forceinline__ void wg_sync() {
+  if constexpr (HALF) half_barrier();
+  else __syncthreads();
 }
 
 // an LDS base pointer through an empty asm (wave-uniform): the carve-up offsets are recomputed per use site on the
@@ -1768,12 +1824,12 @@ __device__ __forceinline__ void team_exchange(const Net& net, const Lds& s, cons
 // one full evaluation.  x_in/tan_in/v_out/tan_out: LDS [MPW][N*D]; t_in: LDS [MPW] (actual time).
 // Must be called by all Geo<NF, NT, P>::NTHR threads of the workgroup (NW waves); returns after a barrier.
 // ---------------------------------------------------------------------------------------------------
-template <int NF, int NT, int L, int D, int P, bool TEAM = false>
+template <int NF, int NT, int L, int D, int P, bool TEAM = false, bool HALF = false>
 __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const float* x_in, const float* t_in, const float* tan_in,
                           float* v_out, float* tan_out, const int* act = nullptr, int sparse_a = -1,
                           float* pcache = nullptr, int pmode = 0, const TeamCtx* tm = nullptr,
                           int* tepoch = nullptr) {
-  constexpr int kNW = Geo<NF, NT, P>::NW, kNT = Geo<NF, NT, P>::NTHR;
+  constexpr int kNW = HALF ? 4 : Geo<NF, NT, P>::NW, kNT = HALF ? 256 : Geo<NF, NT, P>::NTHR;
   constexpr bool kSplitG = Geo<NF, NT, P>::kSplit;
   constexpr bool kSplitN = Geo<NF, NT, P>::kSplitN;   // split node GEMMs (primal split kernels and tangent kernels)
 #ifndef ECNF_NODE_PREFETCH
@@ -1787,7 +1843,7 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
   // tile's spilled 36 B per lane (tests/test_kernel_resources.py).  The BASELINE shapes (LJ13 128/3/3, ALDP 64/2/3,
   // DW4 128/3/2) have it.
   constexpr bool kSparseX = Geo<NF, NT, P>::kL2T && !(L == 2 && (NF == 4 || D == 2));
-  const int tid = opaque_tid(), lane = tid & 63;
+  const int tid = vtid<HALF>(), lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: task indices stay in SGPRs
   const int N = net.N, H = net.H, T = net.T, M = NF * 32, RP = net.RP, MPW = net.MPW, ND = net.ND;
   const int nvalid = MPW * N;
@@ -1807,7 +1863,7 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
     const float arg = ts * net.freqs[k < half ? k : k - half];
     s.temb[idx] = k < half ? sinf(arg) : cosf(arg);
   }
-  __syncthreads();
+  wg_sync<HALF>();
   for (int idx = tid; idx < nvalid * D * (1 + NT); idx += kNT) {
     const int which = idx / (nvalid * D), nd = idx - which * nvalid * D, n = nd / D, d = nd - n * D;
     const int m = n / N;
@@ -1825,7 +1881,7 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
     }
     s.hin[row * s.ld_hin + c] = v;
   }
-  __syncthreads();
+  wg_sync<HALF>();
   STAMP(s, kStPrologue);
 
   const int ntiles = (MPW * net.EP) >> 5;
@@ -1833,7 +1889,7 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
     const BlockW& bw = net.blk[k];
     // fresh (opaque) thread indices per phase group: per-thread addresses of the node phases are then computed after
     // the edge phase instead of being hoisted above it and kept live (spilled) through it
-    int tid = opaque_tid(), lane = tid & 63;
+    int tid = vtid<HALF>(), lane = tid & 63;
     // the last block's h update (gate, aggregation, phi_h) is dead: the field is x_K - x_c - mean (egnn.py:176-188)
     const bool need_h = k + 1 < net.K;
     // split primal kernels: each node GEMM's first A fragments are loaded before the barrier in front of it
@@ -1864,13 +1920,13 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
                                nullptr, 0, s.hb, s.ld_hb, RP, nvalid, kNW - 1 - wave, lane);
       node_gemm<NT, kNW, true>(s.hin, s.ld_hin, H + T, nullptr, 0, 0, bw.Wp, bw.Wp_s, bw.pinv, 2 * M, bw.bnp_u, 2 * M,
                                false, nullptr, 0, s.P, s.ld_P, RP, nvalid, wave, lane);
-      __syncthreads();
+      wg_sync<HALF>();
       STAMP(s, kStNodeDense);
     } else {
     node_gemm<NT, kNW, kSplitN, kPre>(s.hin, s.ld_hin, H + T, nullptr, 0, 0, bw.Wn, bw.Wn_s, bw.ninv, H, bw.bn, H,
                                       false, nullptr, 0, s.hb, s.ld_hb, RP, nvalid, wave, lane, &pre);
     if constexpr (kPre && !Geo<NF, NT, P>::kNoP) node_prefetch<kNW>(bw.Wp_s, H, 0, 2 * M, RP, wave, lane, pre);
-    __syncthreads();
+    wg_sync<HALF>();
     STAMP(s, kStNodeDense);
     // per-node halves of phi_e layer 1 (the M = 256 tangent kernels compute layer 1 per edge)
     if constexpr (!Geo<NF, NT, P>::kNoP) {
@@ -1878,7 +1934,7 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
       node_gemm<NT, kNW, kSplitN, kPre>(s.hb, s.ld_hb, H, nullptr, 0, 0, bw.Wp, bw.Wp_s, bw.pinv, 2 * M,
                                         kPu ? bw.bp_u : bw.bp, 2 * M, false, nullptr, 0, s.P, s.ld_P, RP, nvalid, wave,
                                         lane, &pre);
-      __syncthreads();
+      wg_sync<HALF>();
     }
     }   // !kFusedP
     STAMP(s, kStPGemm);
@@ -1892,7 +1948,7 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
 #endif
 #ifdef ECNF_EXP_BALANCED
     {
-      const int elane = opaque_tid() & 63;
+      const int elane = vtid<HALF>() & 63;
       for (int tile = wave; tile < ntiles_run; tile += kNW) edge_tile<NF, NT, L, D, P>(net, bw, s, tile, elane, need_h);
     }
 #else
@@ -1902,7 +1958,7 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
       // are dealt round-robin over the waves, so a workgroup's tail after its faster molecules finish runs at the
       // cost of the molecules still integrating.  Skipped molecules' outputs are never committed; every molecule's
       // tiles and node rows are its own, so the others' results are unchanged (bitwise).
-      const int elane = opaque_tid() & 63;
+      const int elane = vtid<HALF>() & 63;
       const int tpm = net.EP >> 5;
       unsigned amask = MPW >= 32 ? 0xffffffffu : (1u << MPW) - 1u;
       if (act) {
@@ -1949,7 +2005,10 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
       const int nrun = nd + (pload ? 0 : nact * tpm);
       // team mode (MPW = 1): this member runs tiles t = r, r + G, ... of the molecule (team_exchange)
       const int tstep = TEAM ? tm->p.G : 1, tfirst = TEAM ? tm->r : 0;
-      for (int vt = tfirst + wave * tstep; vt < nrun; vt += kNW * tstep) {
+      // halves mode: the second half deals its tiles from the last wave down, so the SIMD partners w and w + 4 of
+      // the two halves (3, 3, 2, 2 tiles each at 10 tiles) carry 5 tiles per SIMD between them
+      const int dwave = HALF && (threadIdx.x >> 8) ? kNW - 1 - wave : wave;
+      for (int vt = tfirst + dwave * tstep; vt < nrun; vt += kNW * tstep) {
         if constexpr (kSparseX) {
           if (vt < nd) {
             const int q = vt / ndt;
@@ -1971,11 +2030,13 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
 #endif
     constexpr bool kHu0 = kSplitG || Geo<NF, NT, P>::kL2T;   // log2-domain messages, scale in phi_h.0
     if constexpr (kPre)
-      if (need_h) node_prefetch<kNW>(kHu0 ? bw.Wh_s[0] : bw.Wh_sn0, M, H, M, RP, wave, opaque_tid() & 63, pre);
-    __syncthreads();
+      if (need_h) node_prefetch<kNW>(kHu0 ? bw.Wh_s[0] : bw.Wh_sn0, M, H, M, RP, wave, vtid<HALF>() & 63, pre);
+    wg_sync<HALF>();
     if constexpr (TEAM) {   // team mode: rebuild the molecule's aggregates from every member's tiles
+      STAMP(s, kStEdge);
       team_exchange<NT, kNT>(net, s, *tm, *tepoch);
       ++*tepoch;
+      STAMP(s, kStTeam);
     }
     if constexpr (kSparseX) {
       // first JVP pass of an exact-trace evaluation: cache the sparse block's primal aggregates (see the edge loop)
@@ -1990,11 +2051,11 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
           const int m = idx / (N * D);
           pcache[m * pstride + N * M + (k == 0 ? 0 : N * D) + (idx - m * N * D)] = s.dxacc[idx];
         }
-        __syncthreads();
+        wg_sync<HALF>();
       }
     }
     STAMP(s, kStEdge);
-    tid = opaque_tid();
+    tid = vtid<HALF>();
     lane = tid & 63;
     // node update: x += shift_i / (N-1) (egnn.py:95,113); m_i /= sqrt(N-1) (egnn.py:104)
     for (int idx = tid; idx < R * D; idx += kNT) {
@@ -2002,7 +2063,7 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
       s.dxacc[idx] = 0.f;
     }
     if (!need_h) {   // last block: no h update
-      __syncthreads();
+      wg_sync<HALF>();
       STAMP(s, kStNodeUpd);
       continue;
     }
@@ -2025,7 +2086,7 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
         s.macc[row * s.ld_m + c] = s.macc[row * s.ld_m + c] / net.sqrt_nn1;
       }
     }
-    __syncthreads();
+    wg_sync<HALF>();
     if constexpr (kSplitG) {
       if (net.cross) {   // the cross buffer overlaid hin's time-embedding columns: restore them
         for (int idx = tid; idx < nvalid * T; idx += kNT) {
@@ -2040,40 +2101,40 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
       // in place on macc (no P region in these kernels), then macc restarts from +0 for the next block's aggregates
       node_gemm_inplace<NT, kNW>(s.macc, s.ld_m, M, s.hb, s.ld_hb, H, bw.Wh_sn0, bw.hinv_n0, bw.bh[0], M, true,
                                  s.macc, s.ld_m, RP, nvalid, wave, lane);
-      __syncthreads();
+      wg_sync<HALF>();
       for (int l = 1; l < L; ++l) {
         node_gemm_inplace<NT, kNW>(s.macc, s.ld_m, M, nullptr, 0, 0, bw.Wh_s[l], bw.hinv[l], bw.bh[l], M, true, s.macc,
                                    s.ld_m, RP, nvalid, wave, lane);
-        __syncthreads();
+        wg_sync<HALF>();
       }
       node_gemm<NT, kNW, true>(s.macc, s.ld_m, M, nullptr, 0, 0, bw.Wh[L], bw.Wh_s[L], bw.hinv[L], H, bw.bh[L], H, false,
                                s.hb, s.ld_hb, s.hin, s.ld_hin, RP, nvalid, wave, lane);
-      __syncthreads();
+      wg_sync<HALF>();
       for (int idx = tid; idx < R * M; idx += kNT) {
         const int row = idx / M, c = idx - row * M;
         s.macc[row * s.ld_m + c] = 0.f;
       }
-      __syncthreads();
+      wg_sync<HALF>();
       STAMP(s, kStPhiH);
       continue;
     }
     if constexpr (Geo<NF, NT, P>::kWideT32) {   // the same in fp32 (macc already carries the 1 / sqrt(N - 1))
       node_gemm_inplace_f32<NT, kNW>(s.macc, s.ld_m, M, s.hb, s.ld_hb, H, bw.Wh[0], M, bw.bh[0], M, true, s.macc,
                                      s.ld_m, RP, nvalid, wave, lane);
-      __syncthreads();
+      wg_sync<HALF>();
       for (int l = 1; l < L; ++l) {
         node_gemm_inplace_f32<NT, kNW>(s.macc, s.ld_m, M, nullptr, 0, 0, bw.Wh[l], M, bw.bh[l], M, true, s.macc,
                                        s.ld_m, RP, nvalid, wave, lane);
-        __syncthreads();
+        wg_sync<HALF>();
       }
       node_gemm<NT, kNW, false>(s.macc, s.ld_m, M, nullptr, 0, 0, bw.Wh[L], nullptr, 1.0f, H, bw.bh[L], H, false,
                                 s.hb, s.ld_hb, s.hin, s.ld_hin, RP, nvalid, wave, lane);
-      __syncthreads();
+      wg_sync<HALF>();
       for (int idx = tid; idx < R * M; idx += kNT) {
         const int row = idx / M, c = idx - row * M;
         s.macc[row * s.ld_m + c] = 0.f;
       }
-      __syncthreads();
+      wg_sync<HALF>();
       STAMP(s, kStPhiH);
       continue;
     }
@@ -2084,7 +2145,7 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
                                       kHu ? bw.hinv[0] : bw.hinv_n0, M, bw.bh[0], M, true, nullptr, 0, Q0, s.ld_P, RP,
                                       nvalid, wave, lane, &pre);
     if constexpr (kPre) node_prefetch<kNW>(bw.Wh_s[1], M, 0, L == 1 ? H : M, RP, wave, lane, pre);
-    __syncthreads();
+    wg_sync<HALF>();
     if (!(kSplitG && net.cross)) {   // atomically accumulated aggregates restart from +0
       for (int idx = tid; idx < R * M; idx += kNT) {
         const int row = idx / M, c = idx - row * M;
@@ -2095,12 +2156,12 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
       node_gemm<NT, kNW, kSplitN, kPre>(Q0, s.ld_P, M, nullptr, 0, 0, bw.Wh[l], bw.Wh_s[l], bw.hinv[l], M, bw.bh[l], M,
                                         true, nullptr, 0, Q1, s.ld_P, RP, nvalid, wave, lane, &pre);
       if constexpr (kPre) node_prefetch<kNW>(bw.Wh_s[l + 1], M, 0, l + 1 == L ? H : M, RP, wave, lane, pre);
-      __syncthreads();
+      wg_sync<HALF>();
       float* tq = Q0; Q0 = Q1; Q1 = tq;
     }
     node_gemm<NT, kNW, kSplitN, kPre>(Q0, s.ld_P, M, nullptr, 0, 0, bw.Wh[L], bw.Wh_s[L], bw.hinv[L], H, bw.bh[L], H,
                                       false, s.hb, s.ld_hb, s.hin, s.ld_hin, RP, nvalid, wave, lane, &pre);
-    __syncthreads();
+    wg_sync<HALF>();
     STAMP(s, kStPhiH);
   }
 
@@ -2117,7 +2178,7 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
     float* dst = which == 0 ? v_out : tan_out;
     dst[m * ND + (n - m * N) * D + d] = v;
   }
-  __syncthreads();
+  wg_sync<HALF>();
   STAMP(s, kStEpilogue);
 }
 

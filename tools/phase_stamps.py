@@ -15,12 +15,14 @@ from ecnf_amd.engine import EcnfHandle, SolveOptions  # noqa: E402
 
 NAMES = ["prologue", "node_dense", "p_gemm", "edge", "node_update", "phi_h", "epilogue", "solver",
          "edge_chain_e(w0)", "edge_shift(w0)", "edge_layer1(w0)", "edge_gate_agg(w0)", "edge_phix_in(w0)",
-         "edge_phix_chain(w0)"]
+         "edge_phix_chain(w0)", "team_exchange"]
 name = sys.argv[1] if len(sys.argv) > 1 else "lj13"
+TEAM = int(os.environ.get("ECNF_PROBE_TEAM", "0"))   # ecnf_set_team mode for the probe (0 auto)
 B = int(sys.argv[2]) if len(sys.argv) > 2 else 1024
 DIV = sys.argv[3] if len(sys.argv) > 3 else "none"   # none | hutchinson (the tangent kernel)
 cfg = CONFIGS[name]
 h = EcnfHandle(cfg, init_params(cfg, 0), 0)
+h.set_team(TEAM)
 lib = h.lib
 lib.ecnf_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
 z = torch.randn((B, cfg.event_dim), device="cuda")
@@ -39,10 +41,11 @@ torch.cuda.synchronize()
 lib.ecnf_debug_stamps(buf, 32, 1)
 nwg = buf[28]
 cyc = [buf[i] / nwg for i in range(len(NAMES))]
-tot = sum(cyc[:8])
+MAIN = list(range(8)) + [14]   # barrier-delimited phases (incl. the team exchange); 8..13 are edge sub-phases
+tot = sum(cyc[i] for i in MAIN)
 real_us = buf[29] / nwg / 100.0   # s_memrealtime is 100 MHz
 out = {"config": name, "batch": B, "divergence": DIV, "workgroups": nwg, "kernel_ms": ev0.elapsed_time(ev1),
        "cycles_per_wg": tot, "wg_wall_us": real_us, "clock_GHz": tot / (real_us * 1e3),
-       "shares": {n: cyc[i] / tot for i, n in enumerate(NAMES[:8])},
-       "edge_wave0_shares_of_edge": {n: cyc[i] / max(cyc[3], 1) for i, n in list(enumerate(NAMES))[8:]}}
+       "shares": {NAMES[i]: cyc[i] / tot for i in MAIN},
+       "edge_wave0_shares_of_edge": {NAMES[i]: cyc[i] / max(cyc[3], 1) for i in range(8, 14)}}
 print(json.dumps(out, indent=1))
