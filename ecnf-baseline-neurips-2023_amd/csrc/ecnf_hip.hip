@@ -467,6 +467,10 @@ void set_mpw(Net& n, const ecnf_cfg& c, int NT, int P, int mpw, int rp) {
     }
 }
 
+// static LDS of the integrate kernels beside the dynamic carve-up (ecnf_kernels.hpp solver_sizes, egnn_eval.hpp
+// half_bar_words), reserved when a configuration is sized against the CU's 160 KiB
+constexpr size_t kStaticLdsBytes = 64;
+
 int choose_mpw(const ecnf_cfg& c, int NT, int P, int* mpw_out, size_t* lds_out, int* rp_out) {
   const int N = c.n_nodes, D = c.dim, H = c.hidden, T = c.time_embedding_dim, M = c.mlp_width;
   const int E = N * (N - 1), SR = edge_slots_per_receiver(N);
@@ -490,7 +494,7 @@ int choose_mpw(const ecnf_cfg& c, int NT, int P, int* mpw_out, size_t* lds_out, 
                            : lds_eval_floats<0>(N, D, H, T, M, c.mlp_depth, m, RP, vec)) +
                        solver_lds_floats(m, N * D);
     const size_t bytes = (size_t)floats * 4;
-    if (bytes > 160 * 1024) break;
+    if (bytes + kStaticLdsBytes > 160 * 1024) break;
     const int EP = 32 * ((N * SR + 31) / 32);
     const int tiles = m * EP / 32;
     const double eff = (double)tiles / (kSimds * ((tiles + kSimds - 1) / kSimds)) * (double)(m * E) / (tiles * 32.0);
@@ -624,7 +628,7 @@ hipError_t dispatch_integrate(const ecnf_handle* h, int NT, const SolveP& sp_in,
     if (ECNF_HALVES && NT == 0 && split_primal(h->cfg, 0, P) && primal_waves(h->cfg) == 8 && m % 2 == 0) {
       const int mh = m / 2, RP = 32 * ((mh * h->cfg.n_nodes + 31) / 32);
       const size_t lh = lds_bytes(h->cfg, 0, P, mh, RP);
-      if (2 * lh <= 160 * 1024) {
+      if (2 * lh + kStaticLdsBytes <= 160 * 1024) {
         set_mpw(net, h->cfg, 0, P, mh, RP);
         net.lds_floats = (int)(lh / 4);
         lds = lh;

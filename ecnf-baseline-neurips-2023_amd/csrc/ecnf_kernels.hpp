@@ -91,7 +91,23 @@ __device__ __forceinline__ float uniform_f(float x) {
   return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, x)));
 }
 
-__device__ inline float clip_end(float tn, float tau1) { return tn > tau1 - 1e-6f ? tau1 : tn; }
+// the solver loop's sizes (MPW, ND) and the LDS offset of the solver state, in static LDS: written once at the kernel's
+// start and read at every use site in the loop (LDS loads after barriers), so they occupy no SGPRs across the
+// evaluations (kept in SGPRs, they were spilled through VGPRs to scratch in the 256-register kernels)
+__device__ __forceinline__ int* solver_sizes() {
+  __shared__ int sz[4];   // [MPW, ND, solver-state offset in floats from the half's LDS base, -]
+  return sz;
+}
+__device__ __forceinline__ int solver_size(int k) { return __builtin_amdgcn_readfirstlane(solver_sizes()[k]); }
+
+// tau1 passes an empty asm (wave-uniform) so the threshold tau1 - 1e-6 is formed at each use: hoisted out of the solver
+// loop it was a loop-invariant VGPR that spilled in the 256-register kernels
+__device__ inline float clip_end(float tn, float tau1) {
+  int tb = __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, tau1));
+  asm volatile("" : "+s"(tb));
+  const float t1 = __builtin_bit_cast(float, tb);
+  return tn > t1 - 1e-6f ? t1 : tn;
+}
 
 // embedding ids of one molecule (LDS [N]) in [0, n_features)?  Out-of-range ids are replaced by 0 (memory safety).
 __device__ inline bool check_features(const Net& net, int* f) {
@@ -111,7 +127,7 @@ __device__ __forceinline__ void joint_field(const Net& net, const Lds& s, const 
                                             float* kx_out, float* kl_out, const TeamCtx* tm, int* tepoch) {
   constexpr int kThreads = HALF ? 256 : Geo<NF, NT, P>::NTHR;
   // per-thread indices are re-derived (opaque_tid) on each side of the evaluation: kept live across it, they spill
-  const int MPW = opaque_u(net.MPW), ND = opaque_u(net.ND);
+  const int MPW = solver_size(0), ND = solver_size(1);
   int tid = vtid<HALF>();
   // NT == 0: one primal eval; Hutchinson: one JVP along eps; exact: the trace of J from ND - D JVPs along e_k,
   // k >= D.  The field only sees relative positions and subtracts the input mean (egnn.py:176-188), so
@@ -119,7 +135,8 @@ __device__ __forceinline__ void joint_field(const Net& net, const Lds& s, const 
   // {T_c} u {e_k, k >= D} the dual vectors are e_(0,c) and e_k - e_(k mod D), hence
   //   tr J = sum_{k >= D} (J_kk - J_(k mod D),k) - D
   // with J_(k mod D),k the atom-0 component of the same JVP column (D fewer evaluations than the ND unit JVPs).
-  const bool exact = NT && sp.div != ECNF_DIV_HUTCHINSON;
+  // (sp.div re-read through an empty asm at each use: the hoisted flag and -D were loop-invariant VGPRs that spilled)
+  const bool exact = NT && opaque_u(sp.div) != ECNF_DIV_HUTCHINSON;
   const int nrep = exact ? ND - D : 1;
   if (tid < MPW) st.divv[tid] = exact ? -(float)D : 0.f;
   for (int k0 = 0; k0 < nrep; ++k0) {
@@ -129,7 +146,7 @@ __device__ __forceinline__ void joint_field(const Net& net, const Lds& s, const 
       if (sp.div == ECNF_DIV_HUTCHINSON) {
         for (int i = tid; i < MPW * ND; i += kThreads) st.tin[i] = st.eps[i];
       } else {
-        for (int i = tid; i < MPW * ND; i += kThreads) st.tin[i] = ((i % ND) == k) ? 1.0f : 0.0f;
+        for (int i = tid, NDo = opaque_u(ND); i < MPW * NDo; i += kThreads) st.tin[i] = ((i % NDo) == k) ? 1.0f : 0.0f;
       }
       wg_sync<HALF>();
     }
@@ -208,7 +225,6 @@ __global__ __launch_bounds__((HALF ? 512 : Geo<NF, NT, P>::NTHR)) __attribute__(
     if (nmol <= 0) return;   // the second half of the last workgroup has no molecules (it never syncs again)
   ECNF_DCHECK((int)(s.tail - smem) + solver_lds_floats(MPW, ND) <= net.lds_floats, 0);
   ECNF_DCHECK(nmol >= 1 && nmol <= MPW, 5);
-  const bool track = sp.div != ECNF_DIV_NONE;
 
   // zero the eval scratch (aggregates must start at +0; padding rows stay finite)
   for (int i = tid; i < (int)(s.tail - smem); i += kThreads) smem[i] = 0.f;
@@ -231,6 +247,9 @@ __global__ __launch_bounds__((HALF ? 512 : Geo<NF, NT, P>::NTHR)) __attribute__(
     st.tnext[tid] = clip_end(fminf(sp.tau0 + sp.dt0, sp.tau1), sp.tau1);
   }
   if (tid == 0) {
+    solver_sizes()[0] = MPW;
+    solver_sizes()[1] = ND;
+    solver_sizes()[2] = (int)(s.tail - smem);
     // Euler: ConstantStepSize, all molecules share the (uniform) time grid
     st.ctl[0] = __builtin_bit_cast(int, sp.tau0);
     st.ctl[1] = __builtin_bit_cast(int, clip_end(sp.tau0 + sp.dt0, sp.tau1));
@@ -254,8 +273,8 @@ __global__ __launch_bounds__((HALF ? 512 : Geo<NF, NT, P>::NTHR)) __attribute__(
 #endif
   while (true) {
     const int tid = vtid<HALF>();   // shadows the kernel-level tid: nothing per-thread stays live across an eval
-    const int MPW = opaque_u(net.MPW), ND = opaque_u(net.ND);   // (likewise the sizes, the solver-state pointers)
-    const SolverLds st = carve_solver(opaque_smem(s.tail), MPW, ND);
+    const int MPW = solver_size(0), ND = solver_size(1);   // (likewise the sizes, the solver-state pointers)
+    const SolverLds st = carve_solver(smem + solver_size(2), MPW, ND);
     const int a = align4(MPW * ND), b = align4(MPW);
     // the control state, wave-uniform (SGPRs)
     float e_tau = uniform_f(__builtin_bit_cast(float, st.ctl[0])), e_tn = uniform_f(__builtin_bit_cast(float, st.ctl[1]));
@@ -310,8 +329,8 @@ __global__ __launch_bounds__((HALF ? 512 : Geo<NF, NT, P>::NTHR)) __attribute__(
     // per-thread indices, solver pointers and the control state re-derived after the evaluation (nothing of the
     // trip's first half stays live across it)
     const int tid = vtid<HALF>();
-    const int MPW = opaque_u(net.MPW), ND = opaque_u(net.ND);
-    const SolverLds st = carve_solver(opaque_smem(s.tail), MPW, ND);
+    const int MPW = solver_size(0), ND = solver_size(1);
+    const SolverLds st = carve_solver(smem + solver_size(2), MPW, ND);
     const int a = align4(MPW * ND), b = align4(MPW);
     e_tau = uniform_f(__builtin_bit_cast(float, st.ctl[0]));
     e_tn = uniform_f(__builtin_bit_cast(float, st.ctl[1]));
@@ -335,8 +354,8 @@ __global__ __launch_bounds__((HALF ? 512 : Geo<NF, NT, P>::NTHR)) __attribute__(
           sf += (st.kx[tid * ND + c] / sc) * (st.kx[tid * ND + c] / sc);
         }
         const float scl = sp.atol + fabsf(st.lp[tid]) * sp.rtol;
-        const float d0 = rms_state(sy, st.lp[tid] / scl, ND, track);
-        const float d1 = rms_state(sf, st.kl[tid] / scl, ND, track);
+        const float d0 = rms_state(sy, st.lp[tid] / scl, ND, opaque_u(sp.div) != ECNF_DIV_NONE);
+        const float d1 = rms_state(sf, st.kl[tid] / scl, ND, opaque_u(sp.div) != ECNF_DIV_NONE);
         const bool cond = (d0 < 1e-5f) || (d1 < 1e-5f);
         const float d1s = cond ? 1.0f : d1;
         st.h0[tid] = cond ? 1e-6f : 0.01f * (d0 / d1s);
@@ -354,7 +373,7 @@ __global__ __launch_bounds__((HALF ? 512 : Geo<NF, NT, P>::NTHR)) __attribute__(
         const float scl = sp.atol + fabsf(st.lp[tid]) * sp.rtol;
         const float h0 = st.h0[tid];
         const float d1 = st.l1[tid];
-        const float d2 = rms_state(s2, (st.kl[b + tid] - st.kl[tid]) / scl, ND, track) / h0;
+        const float d2 = rms_state(s2, (st.kl[b + tid] - st.kl[tid]) / scl, ND, opaque_u(sp.div) != ECNF_DIV_NONE) / h0;
         const float maxd = fmaxf(d1, d2);
         const float h1 = maxd <= 1e-15f ? fmaxf(1e-6f, h0 * 1e-3f) : powf(0.01f / maxd, 0.2f);
         const float dt = fminf(100.0f * h0, h1);
@@ -393,7 +412,7 @@ __global__ __launch_bounds__((HALF ? 512 : Geo<NF, NT, P>::NTHR)) __attribute__(
           for (int j = 0; j < 7; ++j) el += kBerr[j] * st.kl[j * b + m];
           el = h * el;
           const float scl = sp.atol + fmaxf(fabsf(st.lp[m]), fabsf(l1)) * sp.rtol;
-          const float err = rms_state(ssum, el / scl, ND, track);
+          const float err = rms_state(ssum, el / scl, ND, opaque_u(sp.div) != ECNF_DIV_NONE);
           keep = (err < 1.0f) || st.atmin[m];
           const float inv = 1.0f / err;
           float factor = 0.9f * powf(inv, 0.2f);
@@ -462,7 +481,7 @@ __global__ __launch_bounds__((HALF ? 512 : Geo<NF, NT, P>::NTHR)) __attribute__(
   // re-derived here: kept from the kernel's start, they would stay live across the whole solve and spill.)
   {
   const int tid = vtid<HALF>();
-  const SolverLds st = carve_solver(opaque_smem(s.tail), MPW, ND);
+  const SolverLds st = carve_solver(smem + solver_size(2), MPW, ND);
   if (tid < nmol && st.status[tid] == ECNF_OK) {
     bool fin = isfinite(st.lp[tid]);
     for (int c = 0; c < ND; ++c) fin = fin && isfinite(st.y[tid * ND + c]);

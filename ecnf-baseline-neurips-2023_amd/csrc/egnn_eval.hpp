@@ -380,35 +380,30 @@ __device__ __forceinline__ int vtid() {
   return HALF ? (opaque_tid() & 255) : opaque_tid();
 }
 
-// the barrier of a half: an LDS arrival counter and generation word per half (sense by generation); the LDS writes
+// the barrier of a half: one monotonically increasing LDS arrival counter per half.  Lane 0 of each of the half's 4
+// waves adds 1; barrier n is complete when the counter reaches 4 (n + 1), i.e. 4 more than the multiple of 4 below the
+// value it read (no reset and no generation word, so no ordering between two stores is needed: an earlier form reset
+// the count and then bumped a generation with two relaxed stores, which are free to be reordered).  A wave cannot
+// arrive at barrier n + 1 before all 4 arrived at n, so the counts of consecutive barriers never mix.  The LDS writes
 // of each wave are complete (lgkmcnt(0)) before it arrives.  Never mixed with s_barrier after the kernel's start.
 __device__ __forceinline__ int* half_bar_words() {
-  __shared__ int bar[2][2];   // [half][arrivals, generation]; zeroed at the kernel's start (integrate_kernel)
-  return &bar[0][0];
+  __shared__ int bar[4];   // [half] arrival counters (2 used); zeroed at the kernel's start (integrate_kernel)
+  return bar;
 }
 __device__ __forceinline__ void half_barrier() {
-  int* bar = half_bar_words() + 2 * __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 8));
+  int* bar = half_bar_words() + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 8));
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  const int gen = __builtin_amdgcn_readfirstlane(__hip_atomic_load(bar + 1, __ATOMIC_RELAXED,
-                                                                   __HIP_MEMORY_SCOPE_WORKGROUP));
-  int arrived = 0;
-  if ((threadIdx.x & 63) == 0)
-    arrived = __hip_atomic_fetch_add(bar, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  arrived = __builtin_amdgcn_readfirstlane(arrived);
-  if (arrived == 3) {   // the last of the half's 4 waves: reset the count, then release the generation
-    if ((threadIdx.x & 63) == 0) {
-      __hip_atomic_store(bar, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      __hip_atomic_store(bar + 1, gen + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-  } else {
-    // bounded (seconds): a wave that never arrives would be a bug; the kernel then finishes with wrong results
-    // instead of hanging the device
-    for (unsigned spins = 0; __builtin_amdgcn_readfirstlane(__hip_atomic_load(bar + 1, __ATOMIC_RELAXED,
-                                                                              __HIP_MEMORY_SCOPE_WORKGROUP)) == gen &&
-                             spins < (1u << 26);
-         ++spins)
-      __builtin_amdgcn_s_sleep(1);
-  }
+  int old = 0;
+  if ((threadIdx.x & 63) == 0) old = __hip_atomic_fetch_add(bar, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  const int target = (__builtin_amdgcn_readfirstlane(old) & ~3) + 4;
+  // bounded (seconds): a wave that never arrives would be a bug; the kernel then finishes with wrong results instead
+  // of hanging the device
+  for (unsigned spins = 0; (int)(__builtin_amdgcn_readfirstlane(__hip_atomic_load(bar, __ATOMIC_RELAXED,
+                                                                                   __HIP_MEMORY_SCOPE_WORKGROUP)) -
+                                 target) < 0 &&
+                           spins < (1u << 26);
+       ++spins)
+    __builtin_amdgcn_s_sleep(1);
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
 
@@ -416,15 +411,6 @@ template <bool HALF>
 __device__ __forceinline__ void wg_sync() {
   if constexpr (HALF) half_barrier();
   else __syncthreads();
-}
-
-// an LDS base pointer through an empty asm (wave-uniform): the carve-up offsets are recomputed per use site on the
-// scalar unit instead of occupying SGPRs (and their VGPR spill lanes) across the whole solve
-__device__ __forceinline__ float* opaque_smem(float* p) {
-  uint32_t v = (uint32_t)reinterpret_cast<uintptr_t>(p);
-  v = __builtin_amdgcn_readfirstlane(v);
-  asm volatile("" : "+s"(v));
-  return reinterpret_cast<float*>((uintptr_t)v);
 }
 
 __device__ __forceinline__ f32x4 ldg4(const float* p, int idx4) { return gptr4(p)[idx4]; }
@@ -1147,8 +1133,12 @@ __device__ __forceinline__ void edge_tail(const Net& net, const BlockW& bw, cons
           *reinterpret_cast<f32x4*>(agg_dst + fb * 32 + 8 * q + 4 * kk) =
               f32x4{v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
       } else {
+        // per-lane row base through an empty asm: the 16 constant offsets fold into ds_add_f32's offset field
+        // (otherwise the compiler precomputed the lane addresses once per block and kept them live, i.e. spilled)
+        float* mrow = s.macc + rr * s.ld_m + 4 * kk;
+        asm volatile("" : "+v"(mrow));
 #pragma unroll
-        for (int r16 = 0; r16 < 16; ++r16) lds_add(&s.macc[rr * s.ld_m + fb * 32 + acc_row(r16, kk)], v[r16]);
+        for (int r16 = 0; r16 < 16; ++r16) lds_add(mrow + fb * 32 + acc_row(r16, 0), v[r16]);
       }
     }
     if constexpr (NT) {
@@ -1156,9 +1146,10 @@ __device__ __forceinline__ void edge_tail(const Net& net, const BlockW& bw, cons
       for (int r16 = 0; r16 < 16; ++r16) v[r16] = gT * m[fb][r16] + g * mT[fb][r16];
       sc.sum_many<16, true>(v);
       if (writer) {
+        float* mrow = s.macc + (RP + rr) * s.ld_m + 4 * kk;
+        asm volatile("" : "+v"(mrow));
 #pragma unroll
-        for (int r16 = 0; r16 < 16; ++r16)
-          lds_add(&s.macc[(RP + rr) * s.ld_m + fb * 32 + acc_row(r16, kk)], v[r16]);
+        for (int r16 = 0; r16 < 16; ++r16) lds_add(mrow + fb * 32 + acc_row(r16, 0), v[r16]);
       }
     }
   }
@@ -1850,33 +1841,35 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
   const int R = RP * (1 + NT);
 
   // ---- prologue: input mean, centring (egnn.py:160), embedding (build_cnf.py:79-83) ----
-  for (int idx = tid; idx < MPW * D * (1 + NT); idx += kNT) {
-    const int which = idx / (MPW * D), md = idx - which * MPW * D, m = md / D, d = md - m * D;
+  // (runtime divisors pass opaque_u at each loop: their division constants are formed here instead of being hoisted
+  // above the previous evaluation and kept live, i.e. spilled, across it)
+  for (int idx = tid, MD = opaque_u(MPW * D); idx < MD * (1 + NT); idx += kNT) {
+    const int which = idx / MD, md = idx - which * MD, m = md / D, d = md - m * D;
     const float* src = (which == 0 ? x_in : tan_in) + m * ND + d;
     float acc = 0.f;
     for (int i = 0; i < N; ++i) acc += src[i * D];
     s.mean[idx] = acc / (float)N;
   }
-  for (int idx = tid; idx < MPW * T; idx += kNT) {
-    const int m = idx / T, k = idx - m * T, half = T >> 1;
+  for (int idx = tid, To = opaque_u(T); idx < MPW * To; idx += kNT) {
+    const int m = idx / To, k = idx - m * To, half = To >> 1;
     const float ts = t_in[m] * 1000.0f;                   // build_cnf.py:23
     const float arg = ts * net.freqs[k < half ? k : k - half];
     s.temb[idx] = k < half ? sinf(arg) : cosf(arg);
   }
   wg_sync<HALF>();
-  for (int idx = tid; idx < nvalid * D * (1 + NT); idx += kNT) {
-    const int which = idx / (nvalid * D), nd = idx - which * nvalid * D, n = nd / D, d = nd - n * D;
-    const int m = n / N;
+  for (int idx = tid, VD = opaque_u(nvalid * D), No = opaque_u(N); idx < VD * (1 + NT); idx += kNT) {
+    const int which = idx / VD, nd = idx - which * VD, n = nd / D, d = nd - n * D;
+    const int m = n / No;
     const float* src = which == 0 ? x_in : tan_in;
-    const float v = src[m * ND + (n - m * N) * D + d] - s.mean[which * MPW * D + m * D + d];
+    const float v = src[m * ND + (n - m * No) * D + d] - s.mean[which * MPW * D + m * D + d];
     const int row = which * RP + n;
     s.xc[row * D + d] = v;
   }
-  for (int idx = tid; idx < R * (H + T); idx += kNT) {
-    const int row = idx / (H + T), c = idx - row * (H + T);
+  for (int idx = tid, HT = opaque_u(H + T), No = opaque_u(N); idx < R * HT; idx += kNT) {
+    const int row = idx / HT, c = idx - row * HT;
     float v = 0.f;
     if (row < nvalid) {
-      const int m = row / N;
+      const int m = row / No;
       v = c < H ? gptr(net.emb)[s.feat[row] * H + c] : s.temb[m * T + (c - H)];
     }
     s.hin[row * s.ld_hin + c] = v;

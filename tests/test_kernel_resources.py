@@ -39,12 +39,12 @@ def test_split_kernels_do_not_spill():
     for kind, nf, nt, l, d, p, scratch in ks:
         if p != 0:
             continue   # the strict-fp32 comparator kernels (8 waves of fp32 MFMA chains) are not budgeted here
-        # M = 256 tangent kernels: sequential dual chains at 512 registers keep a few documented spills (DESIGN 3.2;
-        # 48 / 96 B at L = 3 / 4 in round 4); M = 64 tangent kernels at 2 waves per SIMD (256 registers) spill
-        # 24-36 B per lane outside the edge tiles (round 3: 72 B; round 4 re-derives the solver's per-thread indices
-        # and keeps its control state in LDS) and still run 19 % faster than at 1 wave per SIMD with no spill
-        # (egnn_eval.hpp Geo::NW).  Every other split kernel, the team- and halves-mode primal kernels included: 0
-        limit = 96 if (nf == 8 and nt == 1) else 36 if (nf == 2 and nt == 1) else 0
+        # Round 4: every split-precision integrate kernel (batch, team and halves modes, primal and tangent, every M)
+        # runs without scratch; the loop-invariant values that used to spill (division constants of runtime sizes,
+        # the solver's sizes and control flags, the aggregation's lane addresses) are re-derived at their use sites
+        # (opaque_u / solver_size / an opaque row base).  vf_kernel (one evaluation, not the solve loop): the M = 64
+        # tangent form keeps 28 B per lane outside its edge tiles (2 waves per SIMD at 256 registers)
+        limit = 0 if kind == "integrate_kernel" else 28 if (nf == 2 and nt == 1) else 96 if (nf == 8 and nt == 1) else 0
         if scratch > limit:
             bad.append(f"{kind}<{nf},{nt},{l},{d},{p}> scratch {scratch} B/lane (limit {limit})")
     assert not bad, "\n".join(bad)
