@@ -581,8 +581,24 @@ Net net_for_batch(const ecnf_handle* h, int ix, int B, size_t* lds, bool adaptiv
 // leaves most CUs idle.  Auto: one edge-tile round per block (G = ceil(tiles per molecule / waves)) where a round is
 // long against the ~5 us exchange (M = 256: QM9's 36-60 us rounds), B G <= CUs (one member per CU is always
 // co-resident) and B <= team_cap.  ecnf_set_team forces G (>= 2) or turns it off (1).
-int team_size(const ecnf_handle* h, int NT, int B) {
+// floats of the column-split mode's LDS layer image (egnn_eval.hpp edge_tile_cols: NF blocks x 2 k-steps x 2 pieces
+// x 64 lanes x 16 B, the same bytes as the fp32 image NF x 4 x 64 x 16 B)
+int cols_image_floats(const ecnf_cfg& c) { return (c.mlp_width / 32) * 2 * 2 * 64 * 4; }
+
+// Column-split team mode (egnn_eval.hpp edge_tile_cols, M = 256 split primal kernels): G = tiles per molecule, each
+// member runs one tile with its 4 waves split by output block.  Auto mode prefers it when B G <= CUs and the layer
+// image fits the LDS beside the MPW = 1 carve-up.
+bool cols_fits(const ecnf_handle* h, int NT, int B) {
   const ecnf_cfg& c = h->cfg;
+  if (NT != 0 || h->prec != 0 || !cols_shape(c.mlp_width, NT, c.mlp_depth, c.dim, 0)) return false;
+  const int tpm = h->net[0].EP / 32, RP = 32 * ((c.n_nodes + 31) / 32);
+  if (tpm > h->team_gcap || (long)B * tpm > h->ncu) return false;
+  return lds_bytes(c, 0, 0, 1, RP) + (size_t)cols_image_floats(c) * 4 + kStaticLdsBytes <= 160 * 1024;
+}
+
+int team_size(const ecnf_handle* h, int NT, int B, int* cols) {
+  const ecnf_cfg& c = h->cfg;
+  if (cols) *cols = 0;
   if (NT != 0 || B < 1 || B > h->team_cap || h->team_mode == 1 ||
       !team_shape(c.mlp_width, NT, c.mlp_depth, c.dim, h->prec))
     return 1;
@@ -592,6 +608,10 @@ int team_size(const ecnf_handle* h, int NT, int B) {
     G = std::min(std::min(h->team_mode, h->team_gcap), tpm);
   } else {
     if (h->cfg.mlp_width < 256) return 1;
+    if (cols_fits(h, NT, B)) {
+      if (cols) *cols = 1;
+      return tpm;
+    }
     G = std::min((tpm + primal_waves(h->cfg) - 1) / primal_waves(h->cfg), h->team_gcap);
   }
   if (G < 2 || (long)B * G > h->ncu) return 1;
@@ -604,15 +624,21 @@ hipError_t dispatch_integrate(const ecnf_handle* h, int NT, const SolveP& sp_in,
   const int M = h->cfg.mlp_width, L = h->cfg.mlp_depth, D = h->cfg.dim, P = h->prec, ix = 2 * P + NT;
   size_t lds = 0;
   SolveP sp = sp_in;
-  const int G = team_size(h, NT, B);
+  int cols = 0;
+  const int G = team_size(h, NT, B, &cols);
   Net net;
   if (G > 1) {
     net = h->net[ix];
     const int RP = 32 * ((h->cfg.n_nodes + 31) / 32);
     set_mpw(net, h->cfg, NT, P, 1, RP);
     lds = lds_bytes(h->cfg, NT, P, 1, RP);
+    if (cols) {   // the layer image sits before the solver state (carve_lds)
+      net.xs_floats = cols_image_floats(h->cfg);
+      lds += (size_t)net.xs_floats * 4;
+    }
     net.lds_floats = (int)(lds / 4);
     sp.team.G = G;
+    sp.team.cols = cols;
     sp.team.slot = h->team_slot;
     sp.team.buf = h->team_buf;
     sp.team.ctr = h->team_sync;
@@ -1077,7 +1103,8 @@ int ecnf_create(const ecnf_cfg* cfg, const float* params, size_t n_floats, int d
     const Net& n = h->net[0];
     const int tpm = n.EP / 32;
     h->team_cap = kTeamCap;
-    h->team_gcap = std::min(tpm, std::max(4, (tpm + primal_waves(c) - 1) / primal_waves(c)));
+    // (M = 256: room for the column-split mode's G = tiles per molecule)
+    h->team_gcap = c.mlp_width == 256 ? tpm : std::min(tpm, std::max(4, (tpm + primal_waves(c) - 1) / primal_waves(c)));
     h->team_slot = c.n_nodes * M + tpm * M + ((c.n_nodes * c.dim + 3) & ~3);
     const size_t nb = (size_t)h->team_cap * 2 * h->team_gcap * h->team_slot * sizeof(float);
     if (hipMalloc(&h->team_buf, nb) != hipSuccess || hipMalloc(&h->team_sync, kTeamSyncBytes) != hipSuccess) {
@@ -1230,7 +1257,7 @@ int ecnf_set_team(ecnf_handle* h, int32_t mode) {
 
 int ecnf_team_workgroups(ecnf_handle* h, int32_t with_tangent, int32_t batch, int32_t* G) {
   if (!h || !G) return fail(ECNF_E_INVALID, "NULL argument");
-  *G = team_size(h, with_tangent ? 1 : 0, batch);
+  *G = team_size(h, with_tangent ? 1 : 0, batch, nullptr);
   return ECNF_OK;
 }
 
@@ -1324,7 +1351,7 @@ int integrate_impl(ecnf_handle* h, const ecnf_solve_opts* o, const float* y0, co
     HIP_TRY(hipEventRecord(h->arena_ev, stream));
     h->arena_used = true;
     h->arena_stream = stream;
-  } else if (team_size(h, NT, batch) > 1) {
+  } else if (team_size(h, NT, batch, nullptr) > 1) {
     // team mode: the exchange slots and counters are shared by every solve on the handle (ordered as the arena)
     std::lock_guard<std::mutex> tl(h->team_mu);
     if (!h->team_ev) HIP_TRY(hipEventCreateWithFlags(&h->team_ev, hipEventDisableTiming));

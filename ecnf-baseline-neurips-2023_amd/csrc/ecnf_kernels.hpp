@@ -122,7 +122,7 @@ __device__ inline bool check_features(const Net& net, int* f) {
 
 // one evaluation of the joint field g(tau, y) = dir * f(dir * tau, y) at (st.ts, st.ys) for every molecule
 // of the workgroup; writes kx_out [MPW][ND] and kl_out [MPW].  Exactly one egnn_eval call site (it is inlined).
-template <int NF, int NT, int L, int D, int P, bool TEAM, bool HALF>
+template <int NF, int NT, int L, int D, int P, bool TEAM, bool HALF, bool COLS>
 __device__ __forceinline__ void joint_field(const Net& net, const Lds& s, const SolverLds& st, const SolveP& sp,
                                             float* kx_out, float* kl_out, const TeamCtx* tm, int* tepoch) {
   constexpr int kThreads = HALF ? 256 : Geo<NF, NT, P>::NTHR;
@@ -157,7 +157,7 @@ __device__ __forceinline__ void joint_field(const Net& net, const Lds& s, const 
                     ? sp.pcache + (size_t)blockIdx.x * MPW * (net.N * (NF * 32) + 2 * net.N * D)
                     : nullptr;
     ECNF_DCHECK(!pc || (int)(blockIdx.x + 1) * MPW <= sp.pcache_slots, 6);
-    egnn_eval<NF, NT, L, D, P, TEAM, HALF>(net, s, st.ys, st.ts, st.tin, st.vout, st.tout, st.active, sparse ? k / D : -1,
+    egnn_eval<NF, NT, L, D, P, TEAM, HALF, COLS>(net, s, st.ys, st.ts, st.tin, st.vout, st.tout, st.active, sparse ? k / D : -1,
                                      pc, k0 == 0 ? 1 : 2, tm, tepoch);
     tid = vtid<HALF>();
     if constexpr (NT) {
@@ -191,7 +191,7 @@ enum Phase { kEuler = 0, kInit0 = 1, kInit1 = 2, kFsal = 3, kStage = 4 };
 
 // The whole solve as a phase machine around ONE field evaluation per loop trip.  TEAM: the team (latency) mode
 // instantiation (egnn_eval.hpp team_exchange; launched only with sp.team.G > 1, compiled for team_shape)
-template <int NF, int NT, int L, int D, int P, bool TEAM = false, bool HALF = false>
+template <int NF, int NT, int L, int D, int P, bool TEAM = false, bool HALF = false, bool COLS = false>
 __global__ __launch_bounds__((HALF ? 512 : Geo<NF, NT, P>::NTHR)) __attribute__((amdgpu_waves_per_eu(Geo<NF, NT, P>::WPE))) void integrate_kernel(Net net, SolveP sp, const float* __restrict__ y0,
                                                                   const int32_t* __restrict__ feat,
                                                                   const float* __restrict__ eps, float* y1,
@@ -322,7 +322,7 @@ __global__ __launch_bounds__((HALF ? 512 : Geo<NF, NT, P>::NTHR)) __attribute__(
     }
     wg_sync<HALF>();
 
-    joint_field<NF, NT, L, D, P, TEAM, HALF>(net, s, st, sp, kx_out, kl_out, tm, &tepoch);
+    joint_field<NF, NT, L, D, P, TEAM, HALF, COLS>(net, s, st, sp, kx_out, kl_out, tm, &tepoch);
 
     // ------------------------------------------------ consume it
     {
@@ -551,10 +551,12 @@ __global__ __launch_bounds__((Geo<NF, NT, P>::NTHR)) __attribute__((amdgpu_waves
   }
 }
 
-// halves-mode kernels (integrate_kernel HALF): the 8-wave split primal kernels (M <= 128); -DECNF_HALVES=0 builds
-// without them (A/B)
+// halves-mode kernels (integrate_kernel HALF): the 8-wave split primal kernels (M <= 128).  Measured, not adopted
+// (DESIGN 3.10 / 5.3): LJ13 B = 1024 Euler-100 28.17 ms against 26.78 ms for the 8-wave kernel (interleaved A/B), and
+// the ALDP PID sample built with it returned NaNs after barrier timeouts (not investigated further); -DECNF_HALVES=1
+// builds them
 #ifndef ECNF_HALVES
-#define ECNF_HALVES 1
+#define ECNF_HALVES 0
 #endif
 template <int NF, int NT, int P>
 constexpr bool halves_shape() {
@@ -567,6 +569,10 @@ constexpr bool team_shape(int M, int NT, int L, int D, int P) {
   return NT == 0 && P == 0 && D == 3 && ((M == 256 && L == 4) || (M == 128 && L == 3) || (M == 64 && L == 2));
 }
 
+// shapes with a column-split team kernel (egnn_eval.hpp edge_tile_cols): the M = 256 team shape (QM9; 4 waves split
+// its 8 output blocks)
+constexpr bool cols_shape(int M, int NT, int L, int D, int P) { return team_shape(M, NT, L, D, P) && M == 256; }
+
 // ---- templated launchers (one instantiation per compiled shape and tangent flag) ----
 template <int NF, int NT, int L, int D, int P>
 hipError_t launch_integrate(const Net& net, size_t lds, const SolveP& sp, const float* y0, const int32_t* feat,
@@ -577,6 +583,10 @@ hipError_t launch_integrate(const Net& net, size_t lds, const SolveP& sp, const 
     // team mode: the G members of a molecule wait on each other, so the launch must be co-resident; the cooperative
     // launch checks the grid against the occupancy query (hipErrorCooperativeLaunchTooLarge instead of a hang)
     auto kt = integrate_kernel<NF, NT, L, D, P, true>;
+    if constexpr (cols_shape(NF * 32, NT, L, D, P)) {
+      if (sp.team.cols) kt = integrate_kernel<NF, NT, L, D, P, true, false, true>;
+    }
+    if (sp.team.cols && !cols_shape(NF * 32, NT, L, D, P)) return hipErrorInvalidValue;
     hipError_t e = hipFuncSetAttribute((const void*)kt, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     Net n = net;

@@ -181,6 +181,7 @@ struct Net {
   int EP;         // edge slots per molecule (N SR) padded to a multiple of 32 (every molecule starts on a tile boundary)
   int MPW;        // molecules per workgroup
   int lds_floats; // dynamic LDS of one workgroup (device-checked build: ECNF_DCHECK bit 0)
+  int xs_floats;  // column-split team mode (edge_tile_cols): floats of the layer-exchange image (0 otherwise)
   int RP;         // padded primal node rows
   int ND;         // N * D
   float C;        // EGCL normalization constant
@@ -319,6 +320,7 @@ __device__ inline Lds carve_lds(const Net& net, float* base) {
   s.temb = p;  p += align4(net.MPW * net.T);
   s.vecs = p;  p += align4((2 * net.L + 2) * net.M);
   s.feat = reinterpret_cast<int*>(p); p += align4(net.MPW * net.N);
+  p += net.xs_floats;   // column-split team mode's layer image (lds_xs), 0 floats otherwise
 #ifdef ECNF_STAMPS
   s.stamps = reinterpret_cast<unsigned long long*>(p); p += 64;
 #endif
@@ -1133,12 +1135,13 @@ __device__ __forceinline__ void edge_tail(const Net& net, const BlockW& bw, cons
           *reinterpret_cast<f32x4*>(agg_dst + fb * 32 + 8 * q + 4 * kk) =
               f32x4{v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
       } else {
-        // per-lane row base through an empty asm: the 16 constant offsets fold into ds_add_f32's offset field
-        // (otherwise the compiler precomputed the lane addresses once per block and kept them live, i.e. spilled)
-        float* mrow = s.macc + rr * s.ld_m + 4 * kk;
-        asm volatile("" : "+v"(mrow));
+        // per-lane row offset through an empty asm: the 16 constant offsets fold into ds_add_f32's offset field
+        // (otherwise the compiler precomputed the lane addresses once per block and kept them live, i.e. spilled).
+        // The integer, not the pointer, passes the asm: an opaque pointer loses its LDS address space (flat atomics)
+        int mo = rr * s.ld_m + 4 * kk;
+        asm volatile("" : "+v"(mo));
 #pragma unroll
-        for (int r16 = 0; r16 < 16; ++r16) lds_add(mrow + fb * 32 + acc_row(r16, 0), v[r16]);
+        for (int r16 = 0; r16 < 16; ++r16) lds_add(s.macc + mo + fb * 32 + acc_row(r16, 0), v[r16]);
       }
     }
     if constexpr (NT) {
@@ -1146,10 +1149,10 @@ __device__ __forceinline__ void edge_tail(const Net& net, const BlockW& bw, cons
       for (int r16 = 0; r16 < 16; ++r16) v[r16] = gT * m[fb][r16] + g * mT[fb][r16];
       sc.sum_many<16, true>(v);
       if (writer) {
-        float* mrow = s.macc + (RP + rr) * s.ld_m + 4 * kk;
-        asm volatile("" : "+v"(mrow));
+        int mo = (RP + rr) * s.ld_m + 4 * kk;
+        asm volatile("" : "+v"(mo));
 #pragma unroll
-        for (int r16 = 0; r16 < 16; ++r16) lds_add(mrow + fb * 32 + acc_row(r16, 0), v[r16]);
+        for (int r16 = 0; r16 < 16; ++r16) lds_add(s.macc + mo + fb * 32 + acc_row(r16, 0), v[r16]);
       }
     }
   }
@@ -1700,6 +1703,299 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
 }
 
 // ---------------------------------------------------------------------------------------------------
+// Column-split team mode (team cols; the M = 256 split primal kernels, 4 waves): every member workgroup of a
+// molecule's team runs ONE edge tile per block, and its waves split each chain layer of that tile by output block
+// (wave w: blocks [w NJ, (w + 1) NJ), NJ = NF / 4), exchanging the layer through an LDS image (Lds::xs): split pieces
+// in the MFMA B-operand layout between layers, fp32 after a segment's last layer.  Per output element the arithmetic
+// is chain_split's (the same MFMA sequence from the bias column, the same log2-domain SiLU, pair split and fp32 last
+// layer), and the gate / phi_x-output dot products read the whole fp32 layer back and sum in the batch order
+// (edge_tail, edge_shift), so a cols-mode solve is bitwise equal to the batch path's.
+// ---------------------------------------------------------------------------------------------------
+// column-split team mode: the LDS image of one chain layer of the tile, [NF][2][pieces][64] u32x4 split pieces or
+// [NF][4][64] f32x4, right after the feature ids (carve_lds; Net::xs_floats).  Derived from the carve-up where it is
+// used, not held in Lds (one more pointer there spilled in the single-evaluation vf_kernel)
+__device__ __forceinline__ float* lds_xs(const Net& net, const Lds& s) {
+  return reinterpret_cast<float*>(s.feat) + align4(net.MPW * net.N);
+}
+
+// the whole split layer image -> registers (u32x4 [fb][u][piece] at ((fb 2 + u) pieces + piece) 64 + lane)
+template <int NF>
+__device__ __forceinline__ void xs_load(const float* xs, SplitX<NF>& X, int lane) {
+  const u32x4* p = reinterpret_cast<const u32x4*>(xs);
+  static_for<NF>([&](auto Fc) {
+    constexpr int fb = decltype(Fc)::value;
+    static_for<2>([&](auto Uc) {
+      constexpr int u = decltype(Uc)::value;
+      static_for<kPieces>([&](auto Pc) {
+        constexpr int pc = decltype(Pc)::value;
+        X.v[fb][u][pc] = p[((fb * 2 + u) * kPieces + pc) * 64 + lane];
+      });
+    });
+  });
+}
+
+// fp32 accumulator-layout block fb <-> the image (f32x4 [fb][q] at (fb 4 + q) 64 + lane: registers 4q .. 4q + 3)
+__device__ __forceinline__ void mi_store(float* xs, const f32x16& a, int fb, int lane) {
+  f32x4* p = reinterpret_cast<f32x4*>(xs);
+  static_for<4>([&](auto Qc) {
+    constexpr int q = decltype(Qc)::value;
+    p[(fb * 4 + q) * 64 + lane] = f32x4{a[4 * q], a[4 * q + 1], a[4 * q + 2], a[4 * q + 3]};
+  });
+}
+template <int NF>
+__device__ __forceinline__ void mi_load(const float* xs, f32x16 (&m)[NF], int lane) {
+  const f32x4* p = reinterpret_cast<const f32x4*>(xs);
+  static_for<NF>([&](auto Fc) {
+    constexpr int fb = decltype(Fc)::value;
+    static_for<4>([&](auto Qc) {
+      constexpr int q = decltype(Qc)::value;
+      const f32x4 v = p[(fb * 4 + q) * 64 + lane];
+      m[fb][4 * q] = v[0];
+      m[fb][4 * q + 1] = v[1];
+      m[fb][4 * q + 2] = v[2];
+      m[fb][4 * q + 3] = v[3];
+    });
+  });
+}
+
+// one chain layer's MFMAs for this wave's output blocks j0 .. j0 + NJ - 1: acc[jj] = b' + W X.  Wl: the layer's packed
+// split fragments (chain_split's layout: groups (jb, fb, u) output-block major, kPieces x 1 KiB each), lbias: the
+// layer's LDS bias row (log2 domain).  Per block the sequence of chain_split (kBI): C = the bias column, then the
+// k-steps (fb, u) in order, three cross terms each, smallest first.
+template <int NF, int NJ>
+__device__ __forceinline__ void cols_mfma(const SplitX<NF>& X, f32x16 (&acc)[NJ], const unsigned* __restrict__ Wl,
+                                          const float* lbias, int j0, int lane) {
+  constexpr int GB = 2 * NF, NG = NJ * GB, PF = ECNF_SPLIT_PF;
+  const int kk = lane >> 5;
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned*>(Wl), (short)0,
+                                                                         0x7fffffff, 0x00020000);
+  const int voff = lane * 16;
+  const int gbase = __builtin_amdgcn_readfirstlane(j0 * GB);
+  u32x4 wbuf[PF + 1][kPieces];
+  static_for<PF>([&](auto Gc) {
+    constexpr int g = decltype(Gc)::value;
+#pragma unroll
+    for (int p = 0; p < kPieces; ++p) wbuf[g][p] = wload(rsrc, voff, ((gbase + g) * kPieces + p) * kPieceBytes);
+  });
+  static_for<NJ>([&](auto Jc) {
+    constexpr int jj = decltype(Jc)::value;
+    static_for<4>([&](auto Qc) {
+      constexpr int q = decltype(Qc)::value;
+      const f32x4 b4 = *reinterpret_cast<const f32x4*>(lbias + 4 * kk + (j0 + jj) * 32 + 8 * q);
+      acc[jj][4 * q] = b4[0];
+      acc[jj][4 * q + 1] = b4[1];
+      acc[jj][4 * q + 2] = b4[2];
+      acc[jj][4 * q + 3] = b4[3];
+    });
+  });
+  __builtin_amdgcn_s_setprio(ECNF_CHAIN_PRIO);
+  static_for<NG>([&](auto Gc) {
+    constexpr int g = decltype(Gc)::value, jj = g / GB, fb = (g % GB) >> 1, u = g & 1;
+    if constexpr (g + PF < NG) {
+#pragma unroll
+      for (int p = 0; p < kPieces; ++p)
+        wbuf[(g + PF) % (PF + 1)][p] = wload(rsrc, voff, ((gbase + g + PF) * kPieces + p) * kPieceBytes);
+    }
+    static_for<kTerms>([&](auto Tc) {
+      constexpr int t = decltype(Tc)::value;
+      acc[jj] = mfma_split(wbuf[g % (PF + 1)][term_w(t)], X.v[fb][u][term_x(t)], acc[jj]);
+    });
+  });
+  __builtin_amdgcn_s_setprio(0);
+}
+
+// the log2-domain SiLU of this wave's blocks (chain_split stages A-C: y' = u r, r = 1 / (1 + 2^u)); SPLIT: the pairs
+// split into the image's pieces (the next layer's input), else fp32 in place (a segment's last layer)
+template <int NJ, bool SPLIT>
+__device__ __forceinline__ void cols_act(f32x16 (&acc)[NJ], float* xs, int j0, int lane) {
+  u32x4* p = reinterpret_cast<u32x4*>(xs);
+  static_for<NJ>([&](auto Jc) {
+    constexpr int jj = decltype(Jc)::value;
+    static_for<2>([&](auto Uc) {
+      constexpr int u = decltype(Uc)::value;
+      u32x4 w[kPieces];
+      static_for<4>([&](auto Wc) {
+        constexpr int wd = decltype(Wc)::value, r = 8 * u + 2 * wd;
+        const f32x2 uv = {acc[jj][r], acc[jj][r + 1]};
+        f32x2 ev = {__builtin_amdgcn_exp2f(uv[0]), __builtin_amdgcn_exp2f(uv[1])};
+        const f32x2 sv = ev + 1.0f;
+        ev[0] = __builtin_amdgcn_rcpf(sv[0]);
+        ev[1] = __builtin_amdgcn_rcpf(sv[1]);
+        const f32x2 yv = uv * ev;
+        if constexpr (SPLIT) {
+          unsigned pc[kPieces];
+          split_pair(yv[0], yv[1], pc);
+#pragma unroll
+          for (int i = 0; i < kPieces; ++i) w[i][wd] = pc[i];
+        } else {
+          acc[jj][r] = yv[0];
+          acc[jj][r + 1] = yv[1];
+        }
+      });
+      if constexpr (SPLIT) {
+#pragma unroll
+        for (int i = 0; i < kPieces; ++i) p[(((j0 + jj) * 2 + u) * kPieces + i) * 64 + lane] = w[i];
+      }
+    });
+  });
+}
+
+// NL chained layers on the tile (waves split by output block), input: the full split layer X (registers, also in
+// the image); output: the last layer's fp32 activations of EVERY block in m (read back from the image).  Two
+// workgroup barriers per layer: after the MFMAs (every wave has read the image) and after the stores.
+template <int NF, int NL>
+__device__ __forceinline__ void cols_segment(SplitX<NF>& X, f32x16 (&m)[NF], const unsigned* __restrict__ W,
+                                             const float* bias, float* xs, int wave, int lane) {
+  constexpr int NJ = NF / 4, GL = 2 * NF * NF;
+  const int j0 = wave * NJ;
+  f32x16 acc[NJ];
+  static_for<NL>([&](auto Lc) {
+    constexpr int l = decltype(Lc)::value;
+    cols_mfma<NF, NJ>(X, acc, launder_uniform(W + (size_t)l * GL * kPieces * 256), bias + l * NF * 32, j0, lane);
+    __syncthreads();
+    if constexpr (l + 1 < NL) {
+      cols_act<NJ, true>(acc, xs, j0, lane);
+      __syncthreads();
+      xs_load<NF>(xs, X, lane);
+    } else {
+      cols_act<NJ, false>(acc, xs, j0, lane);
+#pragma unroll
+      for (int jj = 0; jj < NJ; ++jj) mi_store(xs, acc[jj], j0 + jj, lane);
+      __syncthreads();
+      mi_load<NF>(xs, m, lane);
+    }
+  });
+}
+
+// one edge tile of the column-split team mode (all waves of the workgroup; NT = 0, split primal kernels, packed
+// receiver runs).  Geometry, layer 1, gate, aggregation and shifts as edge_tile / edge_tail (kSplit path); the
+// aggregation of each message block by the wave that owns it, the shifts stored by wave 0.
+template <int NF, int L, int D>
+__device__ __forceinline__ void edge_tile_cols(const Net& net, const BlockW& bw, const Lds& s, int tile, int wave,
+                                               int lane, bool agg) {
+  static_assert(NF % 4 == 0, "cols mode deals the output blocks over 4 waves");
+  constexpr int NJ = NF / 4, M = NF * 32;
+  const int kk = lane >> 5, li = lane & 31, j0 = wave * NJ;
+  const int N = net.N, nn1 = N - 1;
+  const int mol = (tile * 32) / net.EP;
+  const int e_in = tile * 32 + li - mol * net.EP;
+  const int i0 = e_in / net.SR, jr = e_in - i0 * net.SR;
+  const bool valid = (mol < net.MPW) && (i0 < N) && (jr < nn1);
+  const int i = valid ? i0 : 0;
+  int sd = i + 1 + (valid ? jr : 0);
+  if (sd >= N) sd -= N;
+  const int mrow = valid ? mol : 0;
+  const int rr = mrow * N + i, rs = mrow * N + sd;   // receiver / sender rows (graph.py:10-13)
+  float* agg_dst = nullptr;
+  if (net.cross) {
+    const int tloc = tile - mrow * (net.EP >> 5);
+    agg_dst = tloc == ((i * nn1) >> 5) ? s.macc + rr * s.ld_m : s.cross + (mrow * (net.EP >> 5) + tloc) * s.ld_m;
+  }
+  float r[D], dr[D];
+  float x2 = 0.f;
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    r[d] = s.xc[rr * D + d] - s.xc[rs * D + d];
+    x2 += r[d] * r[d];
+    dr[d] = 0.f;
+  }
+  const bool zero = (x2 == 0.f);
+  const float length = sqrtf(zero ? 1.0f : x2);
+  const float len2 = length * length;
+  float* xs = lds_xs(net, s);
+  // phi_e layer 1 from the per-node halves for this wave's blocks (egnn.py:76,79): u = P_s[s] + P_r[r] + |r|^2 w_d'
+  {
+    const float* Ps = s.P + rs * s.ld_P;
+    const float* Pr = s.P + rr * s.ld_P + M;
+    u32x4* p = reinterpret_cast<u32x4*>(xs);
+    static_for<NJ>([&](auto Jc) {
+      constexpr int jj = decltype(Jc)::value;
+      const int fb = j0 + jj;
+      u32x4 w[2][kPieces];
+      static_for<4>([&](auto Qc) {
+        constexpr int q = decltype(Qc)::value;
+        const int row = fb * 32 + 8 * q + 4 * kk;
+        const f32x4 wv = *reinterpret_cast<const f32x4*>(s.vecs + (2 * L - 1) * (NF * 32) + row);
+        const f32x4 ps = *reinterpret_cast<const f32x4*>(Ps + row);
+        const f32x4 pr = *reinterpret_cast<const f32x4*>(Pr + row);
+        static_for<2>([&](auto Hc) {
+          constexpr int e = 2 * decltype(Hc)::value, R = 4 * q + e, u = R >> 3, wd = (R & 7) >> 1;
+          const float u0 = ps[e] + pr[e] + len2 * wv[e];   // log2 domain (silu_u)
+          const float u1 = ps[e + 1] + pr[e + 1] + len2 * wv[e + 1];
+          unsigned pc[kPieces];
+          split_pair(silu_u(u0), silu_u(u1), pc);
+#pragma unroll
+          for (int k = 0; k < kPieces; ++k) w[u][k][wd] = pc[k];
+        });
+      });
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int k = 0; k < kPieces; ++k) p[((fb * 2 + u) * kPieces + k) * 64 + lane] = w[u][k];
+    });
+  }
+  __syncthreads();
+  SplitX<NF> X;
+  xs_load<NF>(xs, X, lane);
+  f32x16 m[NF];
+  // phi_e layers 2..L
+  cols_segment<NF, L - 1>(X, m, launder_uniform(bw.Ws), s.vecs, xs, wave, lane);
+  SegScan sc;
+  sc.init(valid ? rr : -1, li);
+  const bool writer = valid && sc.tail;
+  if (agg) {
+    // gate e_ij = sigmoid(m_ij . w_g + b_g) over every block, in edge_tail's order (egnn.py:99-101)
+    float part = 0.f;
+#pragma unroll
+    for (int fb = 0; fb < NF; ++fb)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f32x4 w = *reinterpret_cast<const f32x4*>(s.vecs + (2 * L) * (NF * 32) + fb * 32 + 8 * q + 4 * kk);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) part += w[e] * m[fb][4 * q + e];
+      }
+    part += __shfl_xor(part, 32);
+    const float g = sigmoidf_(part + bw.bg);
+    // this wave's message blocks: scatter_sum(m_ij e_ij) (egnn.py:102-104), segment parts stored as edge_tail does
+    static_for<NF>([&](auto Fc) {
+      constexpr int fb = decltype(Fc)::value;
+      if (fb / NJ == wave) {
+        float v[16];
+#pragma unroll
+        for (int r16 = 0; r16 < 16; ++r16) v[r16] = m[fb][r16] * g;
+        sc.sum_many<16, true>(v);
+        if (writer) {
+          if (agg_dst) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+              *reinterpret_cast<f32x4*>(agg_dst + fb * 32 + 8 * q + 4 * kk) =
+                  f32x4{v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
+          } else {
+            int mo = rr * s.ld_m + 4 * kk;
+            asm volatile("" : "+v"(mo));
+#pragma unroll
+            for (int r16 = 0; r16 < 16; ++r16) lds_add(s.macc + mo + fb * 32 + acc_row(r16, 0), v[r16]);
+          }
+        }
+      }
+    });
+  }
+  // phi_x layers 1..L on the (ungated) messages, split in full by every wave
+  static_for<NF>([&](auto Fc) {
+    constexpr int fb = decltype(Fc)::value;
+    static_for<8>([&](auto Ic) {
+      constexpr int k = decltype(Ic)::value;
+      put_pair<NF, fb, 2 * k>(X, m[fb][2 * k], m[fb][2 * k + 1]);
+    });
+  });
+  cols_segment<NF, L>(X, m, launder_uniform(bw.Ws + (size_t)(L - 1) * SplitPlan<NF, 1>::GL * kPieces * 256),
+                      s.vecs + (L - 1) * NF * 32, xs, wave, lane);
+  // phi_x output Dense(1) and the shifts (egnn.py:83-94): every wave computes them, wave 0 stores
+  edge_shift<NF, 0, L, D>(net, bw, s, m, m, writer, sc, rr, r, dr, length, 0.f, lane, wave == 0);
+  __syncthreads();   // the image is rewritten by the next tile's layer 1
+}
+
+// ---------------------------------------------------------------------------------------------------
 // Team (latency) mode: G workgroups integrate ONE molecule together (a batch far below the CU count, e.g. the
 // reference's one-molecule-per-call sampling timer, examples/load_checkpoint_measure_sampling_time.py:101-119).
 // Every member runs the same solver and node phases redundantly (deterministic, so bitwise identical in every
@@ -1724,6 +2020,7 @@ struct TeamP {
   float* buf;          // [molecules][2][G][slot]
   unsigned* ctr;       // [molecules] arrival counters (zeroed before every launch)
   int* timeout;        // [molecules] set when an exchange timed out (zeroed before every launch)
+  int cols;            // 1: column-split mode (edge_tile_cols; G = tiles per molecule, one tile per member)
 };
 
 struct TeamCtx {
@@ -1815,7 +2112,7 @@ __device__ __forceinline__ void team_exchange(const Net& net, const Lds& s, cons
 // one full evaluation.  x_in/tan_in/v_out/tan_out: LDS [MPW][N*D]; t_in: LDS [MPW] (actual time).
 // Must be called by all Geo<NF, NT, P>::NTHR threads of the workgroup (NW waves); returns after a barrier.
 // ---------------------------------------------------------------------------------------------------
-template <int NF, int NT, int L, int D, int P, bool TEAM = false, bool HALF = false>
+template <int NF, int NT, int L, int D, int P, bool TEAM = false, bool HALF = false, bool COLS = false>
 __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const float* x_in, const float* t_in, const float* tan_in,
                           float* v_out, float* tan_out, const int* act = nullptr, int sparse_a = -1,
                           float* pcache = nullptr, int pmode = 0, const TeamCtx* tm = nullptr,
@@ -1998,6 +2295,14 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
       const int nrun = nd + (pload ? 0 : nact * tpm);
       // team mode (MPW = 1): this member runs tiles t = r, r + G, ... of the molecule (team_exchange)
       const int tstep = TEAM ? tm->p.G : 1, tfirst = TEAM ? tm->r : 0;
+      if constexpr (COLS) {
+        // column-split team mode: member r runs tile r (G = tiles per molecule) with all of its waves
+        static_assert(TEAM && NT == 0 && Geo<NF, NT, P>::kSplit, "cols mode: team primal split kernels");
+        for (int vt = tfirst; vt < nrun; vt += tstep) {
+          const int q = vt / tpm;
+          edge_tile_cols<NF, L, D>(net, bw, s, nth_active(q) * tpm + (vt - q * tpm), wave, elane, need_h);
+        }
+      } else {
       // halves mode: the second half deals its tiles from the last wave down, so the SIMD partners w and w + 4 of
       // the two halves (3, 3, 2, 2 tiles each at 10 tiles) carry 5 tiles per SIMD between them
       const int dwave = HALF && (threadIdx.x >> 8) ? kNW - 1 - wave : wave;
@@ -2019,6 +2324,7 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
         }
         edge_tile<NF, NT, L, D, P>(net, bw, s, tile, elane, need_h);
       }
+      }   // !COLS
     }
 #endif
     constexpr bool kHu0 = kSplitG || Geo<NF, NT, P>::kL2T;   // log2-domain messages, scale in phi_h.0

@@ -40,8 +40,18 @@ def test_team_sizes():
     for batches up to 32 (B G <= CUs); the M <= 128 shapes keep the batch path unless forced; divergence solves and
     shapes without a team kernel always run the batch path."""
     _, _, hq, _, _, _ = setup(CONFIGS["qm9"], B=1)
-    assert hq.team_workgroups(1) == 7 and hq.team_workgroups(32) == 7
+    # column-split mode (edge_tile_cols: one tile per member, G = 26 tiles) while B x 26 fits the CUs, then the
+    # tile-dealt mode (G = 7)
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    bc = ncu // 26
+    assert hq.team_workgroups(1) == 26 and hq.team_workgroups(bc) == 26
+    assert hq.team_workgroups(bc + 1) == 7 and hq.team_workgroups(32) == 7
     assert hq.team_workgroups(33) == 1 and hq.team_workgroups(1, with_tangent=True) == 1
+    hq.set_team(7)   # forced: the tile-dealt mode
+    try:
+        assert hq.team_workgroups(1) == 7
+    finally:
+        hq.set_team(0)
     _, _, hl, _, _, _ = setup(CONFIGS["lj13"], B=1)
     assert hl.team_workgroups(1) == 1
     hl.set_team(3)
@@ -60,8 +70,11 @@ def test_team_sizes():
 
 
 @pytest.mark.parametrize("name,B,mode,opts", [
-    ("qm9", 1, 0, SolveOptions("euler", 0.1)),
+    ("qm9", 1, 0, SolveOptions("euler", 0.1)),      # column-split mode (G = 26)
     ("qm9", 3, 0, SolveOptions("euler", 0.2)),
+    ("qm9", 9, 0, SolveOptions("dopri5", 0.25)),
+    ("qm9", 1, 7, SolveOptions("euler", 0.1)),      # tile-dealt mode (forced G = 7)
+    ("qm9", 12, 0, SolveOptions("euler", 0.25)),    # auto, past the column-split mode's CU budget: G = 7
     ("qm9", 2, 4, SolveOptions("dopri5", 0.25)),
     ("qm9", 1, 0, SolveOptions("dopri5", None)),
     ("lj13", 3, 2, SolveOptions("euler", 0.05)),
@@ -88,7 +101,7 @@ def test_team_qm9_one_molecule_vs_oracle_and_surface():
     (Euler, 10 steps, 1e-4 as test_euler_sample_short); the default adaptive call reports a plausible NFE."""
     cfg = CONFIGS["qm9"]
     oc, params, h, z, x0, feat = setup(cfg, B=1)
-    assert h.team_workgroups(1) == 7
+    assert h.team_workgroups(1) == 26
     cnf = C.build_cnf(n_frames=cfg.n_nodes, dim=cfg.dim, sigma_min=cfg.sigma_min, base_scale=cfg.base_scale,
                       n_blocks_egnn=cfg.n_blocks, mlp_units=(cfg.mlp_width,) * cfg.mlp_depth,
                       n_invariant_feat_hidden=cfg.hidden, time_embedding_dim=cfg.time_embedding_dim,

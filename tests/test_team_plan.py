@@ -8,7 +8,7 @@ tiles, (2) every edge tile belongs to exactly one member (t mod G), and (3) a me
 tiles contributes nothing for it.  This test restates the edge layout (graph.py:6-14 receiver-major, packed for
 N <= 33, receiver-tiled with 64 slots per receiver beyond) and the plan's index rules in numpy and checks those
 properties, and that summing the owners' parts in the plan's order reproduces a single workgroup's sums bitwise for
-random fp32 edge values, for every N in 2 ... 64 and G in 2 ... 8."""
+random fp32 edge values, for every N in 2 ... 64 and G in 2 ... 8 or G = the tiles per molecule."""
 import numpy as np
 import pytest
 
@@ -38,7 +38,9 @@ def test_receiver_segments_touch_at_most_two_consecutive_tiles(n):
         assert t == set(range(first_tile(i, n), last_tile(i, n) + 1)) and len(t) <= 2
 
 
-@pytest.mark.parametrize("n,G", [(n, G) for n in (2, 4, 5, 13, 19, 22, 29, 33, 34, 40, 64) for G in range(2, 9)])
+# G in 2 ... 8 (the tile-dealt mode) and G = tiles per molecule (the column-split mode, one tile per member)
+@pytest.mark.parametrize("n,G", [(n, G) for n in (2, 4, 5, 13, 19, 22, 29, 33, 34, 40, 64)
+                                 for G in sorted(set(range(2, 9)) | {max(2, tiles(n))})])
 def test_rebuilt_aggregates_equal_single_workgroup(n, G):
     rng = np.random.default_rng(n * 10 + G)
     sr = slots_per_receiver(n)

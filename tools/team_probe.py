@@ -28,10 +28,11 @@ for B in batches:
     steps = 20
     rows = {}
     ref = None
-    for mode in (1, 2, 3, 4, 5, 7, 9, 13):
+    for mode in (1, 0, 2, 4, 7, 13):   # 1: batch path, 0: auto (QM9 B <= 9: column-split, G = 26), >= 2: tile-dealt
         h.set_team(mode)
         G = h.team_workgroups(B)
-        if mode > 1 and (G == 1 or str(G) in rows):
+        key = f"{'auto' if mode == 0 else 'forced'}_G{G}"
+        if mode != 1 and (G == 1 or key in rows):
             continue
         y, _, _, _ = h.integrate(x0, feat, 0.0, 1.0, SolveOptions("euler", 1.0 / steps))
         ref = y if ref is None else ref
@@ -44,7 +45,7 @@ for B in batches:
             torch.cuda.synchronize()
             ts.append(a.elapsed_time(b))
         ms = sorted(ts)[2]
-        rows[str(G)] = {"kernel_ms": ms, "us_per_eval": 1e3 * ms / steps, "bitwise_vs_batch": bool(torch.equal(y, ref))}
+        rows[key] = {"kernel_ms": ms, "us_per_eval": 1e3 * ms / steps, "bitwise_vs_batch": bool(torch.equal(y, ref))}
     h.set_team(0)
     # the reference timer's call: PID, one molecule, host copy
     walls, nfes = [], []
