@@ -1758,52 +1758,6 @@ __device__ __forceinline__ void mi_load(const float* xs, f32x16 (&m)[NF], int la
   });
 }
 
-// one chain layer's MFMAs for this wave's output blocks j0 .. j0 + NJ - 1: acc[jj] = b' + W X.  Wl: the layer's packed
-// split fragments (chain_split's layout: groups (jb, fb, u) output-block major, kPieces x 1 KiB each), lbias: the
-// layer's LDS bias row (log2 domain).  Per block the sequence of chain_split (kBI): C = the bias column, then the
-// k-steps (fb, u) in order, three cross terms each, smallest first.
-template <int NF, int NJ>
-__device__ __forceinline__ void cols_mfma(const SplitX<NF>& X, f32x16 (&acc)[NJ], const unsigned* __restrict__ Wl,
-                                          const float* lbias, int j0, int lane) {
-  constexpr int GB = 2 * NF, NG = NJ * GB, PF = ECNF_SPLIT_PF;
-  const int kk = lane >> 5;
-  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned*>(Wl), (short)0,
-                                                                         0x7fffffff, 0x00020000);
-  const int voff = lane * 16;
-  const int gbase = __builtin_amdgcn_readfirstlane(j0 * GB);
-  u32x4 wbuf[PF + 1][kPieces];
-  static_for<PF>([&](auto Gc) {
-    constexpr int g = decltype(Gc)::value;
-#pragma unroll
-    for (int p = 0; p < kPieces; ++p) wbuf[g][p] = wload(rsrc, voff, ((gbase + g) * kPieces + p) * kPieceBytes);
-  });
-  static_for<NJ>([&](auto Jc) {
-    constexpr int jj = decltype(Jc)::value;
-    static_for<4>([&](auto Qc) {
-      constexpr int q = decltype(Qc)::value;
-      const f32x4 b4 = *reinterpret_cast<const f32x4*>(lbias + 4 * kk + (j0 + jj) * 32 + 8 * q);
-      acc[jj][4 * q] = b4[0];
-      acc[jj][4 * q + 1] = b4[1];
-      acc[jj][4 * q + 2] = b4[2];
-      acc[jj][4 * q + 3] = b4[3];
-    });
-  });
-  __builtin_amdgcn_s_setprio(ECNF_CHAIN_PRIO);
-  static_for<NG>([&](auto Gc) {
-    constexpr int g = decltype(Gc)::value, jj = g / GB, fb = (g % GB) >> 1, u = g & 1;
-    if constexpr (g + PF < NG) {
-#pragma unroll
-      for (int p = 0; p < kPieces; ++p)
-        wbuf[(g + PF) % (PF + 1)][p] = wload(rsrc, voff, ((gbase + g + PF) * kPieces + p) * kPieceBytes);
-    }
-    static_for<kTerms>([&](auto Tc) {
-      constexpr int t = decltype(Tc)::value;
-      acc[jj] = mfma_split(wbuf[g % (PF + 1)][term_w(t)], X.v[fb][u][term_x(t)], acc[jj]);
-    });
-  });
-  __builtin_amdgcn_s_setprio(0);
-}
-
 // the log2-domain SiLU of this wave's blocks (chain_split stages A-C: y' = u r, r = 1 / (1 + 2^u)); SPLIT: the pairs
 // split into the image's pieces (the next layer's input), else fp32 in place (a segment's last layer)
 template <int NJ, bool SPLIT>
@@ -1840,29 +1794,73 @@ __device__ __forceinline__ void cols_act(f32x16 (&acc)[NJ], float* xs, int j0, i
   });
 }
 
-// NL chained layers on the tile (waves split by output block), input: the full split layer X (registers, also in
-// the image); output: the last layer's fp32 activations of EVERY block in m (read back from the image).  Two
-// workgroup barriers per layer: after the MFMAs (every wave has read the image) and after the stores.
+#ifndef ECNF_COLS_PF
+#define ECNF_COLS_PF 8   // weight groups in flight per wave in the column-split chain (its fragments come from L2)
+#endif
+// NL chained layers on the tile, the waves split by output block (wave w: blocks j0 .. j0 + NJ - 1, j0 = w NJ).
+// Input: the full split layer X (registers; also in the image); output: the last layer's fp32 activations of EVERY
+// block in m (read back from the image).  Per layer and block the MFMA sequence of chain_split (kBI: C = the bias
+// column, then the k-steps (fb, u) in order, three cross terms each, smallest first) and its activation; two
+// workgroup barriers per layer (after the MFMAs: every wave has read the image; after the stores).  The wave's
+// weight groups (chain_split's packed layout: [layer][jb][fb][u][piece], 1 KiB per piece) stream as ONE sequence over
+// the layers, ECNF_COLS_PF groups ahead, so the next layer's first fragments are in flight across the barriers and
+// the activation (each wave reads its own blocks' fragments from L2: nothing is shared in L1 as in the batch path).
 template <int NF, int NL>
 __device__ __forceinline__ void cols_segment(SplitX<NF>& X, f32x16 (&m)[NF], const unsigned* __restrict__ W,
                                              const float* bias, float* xs, int wave, int lane) {
-  constexpr int NJ = NF / 4, GL = 2 * NF * NF;
-  const int j0 = wave * NJ;
-  f32x16 acc[NJ];
-  static_for<NL>([&](auto Lc) {
-    constexpr int l = decltype(Lc)::value;
-    cols_mfma<NF, NJ>(X, acc, launder_uniform(W + (size_t)l * GL * kPieces * 256), bias + l * NF * 32, j0, lane);
-    __syncthreads();
-    if constexpr (l + 1 < NL) {
-      cols_act<NJ, true>(acc, xs, j0, lane);
-      __syncthreads();
-      xs_load<NF>(xs, X, lane);
-    } else {
-      cols_act<NJ, false>(acc, xs, j0, lane);
+  constexpr int NJ = NF / 4, GB = 2 * NF, GL = GB * NF, NG = NJ * GB, NQ = NL * NG, PF = ECNF_COLS_PF;
+  const int j0 = wave * NJ, kk = lane >> 5;
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned*>(W), (short)0,
+                                                                         0x7fffffff, 0x00020000);
+  const int voff = lane * 16;
+  const int gbase = __builtin_amdgcn_readfirstlane(j0 * GB);   // this wave's first group of a layer
+  // byte offset of the wave's q-th group: layer q / NG, its group q % NG from gbase
+  auto woff = [&](int q) { return (((q / NG) * GL + gbase + (q % NG)) * kPieces) * kPieceBytes; };
+  u32x4 wbuf[PF + 1][kPieces];
+  static_for<PF>([&](auto Qc) {
+    constexpr int q = decltype(Qc)::value;
 #pragma unroll
-      for (int jj = 0; jj < NJ; ++jj) mi_store(xs, acc[jj], j0 + jj, lane);
+    for (int p = 0; p < kPieces; ++p) wbuf[q][p] = wload(rsrc, voff, woff(q) + p * kPieceBytes);
+  });
+  f32x16 acc[NJ];
+  static_for<NQ>([&](auto Qc) {
+    constexpr int q = decltype(Qc)::value, l = q / NG, g = q % NG, jj = g / GB, fb = (g % GB) >> 1, u = g & 1;
+    if constexpr (g == 0) {   // the layer's accumulators start at its bias column (chain_split kBI)
+      static_for<NJ>([&](auto Jc) {
+        constexpr int j = decltype(Jc)::value;
+        static_for<4>([&](auto Rc) {
+          constexpr int r4 = decltype(Rc)::value;
+          const f32x4 b4 = *reinterpret_cast<const f32x4*>(bias + l * NF * 32 + 4 * kk + (j0 + j) * 32 + 8 * r4);
+          acc[j][4 * r4] = b4[0];
+          acc[j][4 * r4 + 1] = b4[1];
+          acc[j][4 * r4 + 2] = b4[2];
+          acc[j][4 * r4 + 3] = b4[3];
+        });
+      });
+      __builtin_amdgcn_s_setprio(ECNF_CHAIN_PRIO);
+    }
+    if constexpr (q + PF < NQ) {
+#pragma unroll
+      for (int p = 0; p < kPieces; ++p) wbuf[(q + PF) % (PF + 1)][p] = wload(rsrc, voff, woff(q + PF) + p * kPieceBytes);
+    }
+    static_for<kTerms>([&](auto Tc) {
+      constexpr int t = decltype(Tc)::value;
+      acc[jj] = mfma_split(wbuf[q % (PF + 1)][term_w(t)], X.v[fb][u][term_x(t)], acc[jj]);
+    });
+    if constexpr (g == NG - 1) {   // the layer's MFMAs are issued: activation and exchange
+      __builtin_amdgcn_s_setprio(0);
       __syncthreads();
-      mi_load<NF>(xs, m, lane);
+      if constexpr (l + 1 < NL) {
+        cols_act<NJ, true>(acc, xs, j0, lane);
+        __syncthreads();
+        xs_load<NF>(xs, X, lane);
+      } else {
+        cols_act<NJ, false>(acc, xs, j0, lane);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) mi_store(xs, acc[j], j0 + j, lane);
+        __syncthreads();
+        mi_load<NF>(xs, m, lane);
+      }
     }
   });
 }

@@ -1,0 +1,15 @@
+# round-4: the whole GPU suite and smoke at the product build, then phase stamps of the QM9 one-molecule team modes
+# (column-split auto / tile-dealt G = 7) and of ALDP B = 512 (primal and Hutchinson) (gpurun_out/r4k/)
+cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out/r4k && export TMPDIR=/tmp && \
+timeout -k 5 150 python -u tools/diag_small.py dw4 lj13 aldp qm9 > gpurun_out/r4k/diag.log 2>&1; rc=$?; grep -c " ok " gpurun_out/r4k/diag.log; \
+[ $rc -eq 0 ] || { cat gpurun_out/r4k/diag.log; exit $rc; }; \
+timeout -k 10 700 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/r4k/pytest.log 2>&1; rc=$?; tail -3 gpurun_out/r4k/pytest.log; \
+[ $rc -eq 0 ] || exit $rc; \
+timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r4k/smoke.log 2>&1 && cat gpurun_out/r4k/smoke.log && \
+ECNF_STAMPS_LIB=tools/libecnf_hip_stamps_qm9.so timeout -k 10 120 python -u tools/phase_stamps.py qm9 1 > gpurun_out/r4k/stamps_qm9_cols.json 2>&1 && \
+ECNF_PROBE_TEAM=7 ECNF_STAMPS_LIB=tools/libecnf_hip_stamps_qm9.so timeout -k 10 120 python -u tools/phase_stamps.py qm9 1 > gpurun_out/r4k/stamps_qm9_g7.json 2>&1 && \
+ECNF_STAMPS_LIB=tools/libecnf_hip_stamps_aldp.so timeout -k 10 120 python -u tools/phase_stamps.py aldp 512 > gpurun_out/r4k/stamps_aldp.json 2>&1 && \
+ECNF_STAMPS_LIB=tools/libecnf_hip_stamps_aldp.so timeout -k 10 120 python -u tools/phase_stamps.py aldp 512 hutchinson > gpurun_out/r4k/stamps_aldp_hutch.json 2>&1 && \
+cat gpurun_out/r4k/stamps_qm9_cols.json gpurun_out/r4k/stamps_qm9_g7.json | grep -v amdgpu.ids; \
+timeout -k 10 200 python -u tools/team_probe.py qm9 1 > gpurun_out/r4k/team_qm9.log 2>&1; tail -c 1200 gpurun_out/r4k/team_qm9.log; \
+bash tools/pmc_issue.sh r4k; tail -3 gpurun_out/prof_r4k/issue.log
