@@ -54,6 +54,13 @@ constexpr bool kSplitTanChain = kSplitChain;
 #define ECNF_SPLIT_MAX_NF 8
 #endif
 constexpr int kSplitMaxNF = ECNF_SPLIT_MAX_NF;   // split chain up to M = 32 kSplitMaxNF
+// k-steps of node-GEMM A fragments in flight (node_task_split; Geo::kNodePFA)
+#ifndef ECNF_NODE_PFA_WIDE   // (A/B pending: 6 for the M = 256 split primal kernels, tools/libt_q6 vs libt_q2)
+#define ECNF_NODE_PFA_WIDE 2
+#endif
+#ifndef ECNF_NODE_PFA
+#define ECNF_NODE_PFA 2
+#endif
 // Tangent kernels' node GEMMs (node Dense, the phi_e.0 halves, phi_h) on the split path; -DECNF_FP32_TANGENT_NODE
 // keeps them on v_mfma_f32_32x32x2_f32.
 #ifdef ECNF_FP32_TANGENT_NODE
@@ -112,6 +119,10 @@ struct Geo {
   // split primal kernels at -DECNF_SPLIT_NW=4.  (The M = 256 split primal kernels also run 4 waves, but need their
   // 512 registers: at 2 waves per SIMD they spilled 968 B per lane and QM9 B = 2048 Euler-100 ran 2162 -> 3423 ms.)
   static constexpr int WPE = ((kSplit && NF <= 4 && NW == 4) || (NT == 1 && NW == 8)) ? 2 : 1;
+  // k-steps of node-GEMM A fragments in flight (node_task_split): the M = 256 split primal kernels (4 waves, 512
+  // registers; their node GEMMs stream 64 KiB of fragments per wave from L2 per GEMM: QM9's latency path is made of
+  // them) run a deeper ring than the 256-register kernels
+  static constexpr int kNodePFA = (kSplit && NF == 8) ? ECNF_NODE_PFA_WIDE : ECNF_NODE_PFA;
 };
 constexpr int kMaxBlocks = 10;
 constexpr int kMaxPhiH = 5;     // L + 1 <= 5
@@ -553,9 +564,7 @@ __device__ __forceinline__ void node_task(const float* X1, int ldx1, int K1, con
 // shares every A fragment and gets no bias, act'(pre) * (X_T W) (as node_task).
 // INPLACE (Y may alias X1): every wave of the workgroup calls it once (active = false: no task) and the outputs are
 // written after a barrier that follows every wave's k-loop.
-#ifndef ECNF_NODE_PFA
-#define ECNF_NODE_PFA 2
-#endif
+
 // the first ECNF_NODE_PFA k-steps of a node GEMM task's A fragments, loaded before the barrier that precedes the GEMM
 // (node_prefetch): the weights do not depend on the phase's inputs, so their L2 latency overlaps the barrier wait and
 // the previous phase's tail instead of opening every node phase
@@ -563,13 +572,14 @@ struct NodePre {
   u32x4 w[ECNF_NODE_PFA][2][kPieces];
 };
 
-template <int NA, int NT = 0, bool INPLACE = false, bool PRE = false>
+template <int NA, int NT = 0, bool INPLACE = false, bool PRE = false, int PFA = ECNF_NODE_PFA>
 __device__ __forceinline__ void node_task_split(const float* X1, int ldx1, int K1, const float* X2, int ldx2, int K2,
                                                 const unsigned* __restrict__ Wpk, float winv,
                                                 const float* __restrict__ bias, bool act, const float* resid, int ldr, float* Y, int ldy, int RP,
                                                 int nvalid, int jb, int ct, int lane, bool active = true,
                                                 const NodePre* pre = nullptr) {
-  constexpr int PFA = ECNF_NODE_PFA;   // k-steps of A fragments in flight ahead of the MFMAs
+  // PFA: k-steps of A fragments in flight ahead of the MFMAs (the prefetched first k-steps of PRE are ECNF_NODE_PFA)
+  static_assert(!PRE || PFA == ECNF_NODE_PFA, "node_prefetch fills ECNF_NODE_PFA k-steps");
   jb = __builtin_amdgcn_readfirstlane(jb);   // uniform: buffer-load offsets in SGPRs (no waterfall loops)
   ct = __builtin_amdgcn_readfirstlane(ct);
   const int kk = lane >> 5, li = lane & 31;
@@ -752,7 +762,7 @@ __device__ __forceinline__ void node_prefetch(const unsigned* __restrict__ Ws, i
   });
 }
 
-template <int NT, int NW, bool SPLIT, bool PRE = false>
+template <int NT, int NW, bool SPLIT, bool PRE = false, int PFA = ECNF_NODE_PFA>
 __device__ __forceinline__ void node_gemm(const float* X1, int ldx1, int K1, const float* X2, int ldx2, int K2,
                                           const float* __restrict__ W, const unsigned* __restrict__ Ws, float winv,
                                           int ldw, const float* __restrict__ bias, int NOUT, bool act, const float* resid,
@@ -770,7 +780,7 @@ __device__ __forceinline__ void node_gemm(const float* X1, int ldx1, int K1, con
         task += NW;
       }
       for (; task < npair * nct; task += NW)
-        node_task_split<2, NT>(X1, ldx1, K1, X2, ldx2, K2, Ws, winv, bias, act, resid, ldr, Y, ldy, RP, nvalid,
+        node_task_split<2, NT, false, false, PFA>(X1, ldx1, K1, X2, ldx2, K2, Ws, winv, bias, act, resid, ldr, Y, ldy, RP, nvalid,
                                2 * (task % npair), task / npair, lane);
     } else {
       int task = wave;
@@ -781,7 +791,7 @@ __device__ __forceinline__ void node_gemm(const float* X1, int ldx1, int K1, con
         task += NW;
       }
       for (; task < njb * nct; task += NW)
-        node_task_split<1, NT>(X1, ldx1, K1, X2, ldx2, K2, Ws, winv, bias, act, resid, ldr, Y, ldy, RP, nvalid,
+        node_task_split<1, NT, false, false, PFA>(X1, ldx1, K1, X2, ldx2, K2, Ws, winv, bias, act, resid, ldr, Y, ldy, RP, nvalid,
                                task % njb, task / njb, lane);
     }
     return;
@@ -2211,7 +2221,7 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
       wg_sync<HALF>();
       STAMP(s, kStNodeDense);
     } else {
-    node_gemm<NT, kNW, kSplitN, kPre>(s.hin, s.ld_hin, H + T, nullptr, 0, 0, bw.Wn, bw.Wn_s, bw.ninv, H, bw.bn, H,
+    node_gemm<NT, kNW, kSplitN, kPre, Geo<NF, NT, P>::kNodePFA>(s.hin, s.ld_hin, H + T, nullptr, 0, 0, bw.Wn, bw.Wn_s, bw.ninv, H, bw.bn, H,
                                       false, nullptr, 0, s.hb, s.ld_hb, RP, nvalid, wave, lane, &pre);
     if constexpr (kPre && !Geo<NF, NT, P>::kNoP) node_prefetch<kNW>(bw.Wp_s, H, 0, 2 * M, RP, wave, lane, pre);
     wg_sync<HALF>();
@@ -2219,7 +2229,7 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
     // per-node halves of phi_e layer 1 (the M = 256 tangent kernels compute layer 1 per edge)
     if constexpr (!Geo<NF, NT, P>::kNoP) {
       constexpr bool kPu = kSplitG || Geo<NF, NT, P>::kL2T;   // log2-domain P
-      node_gemm<NT, kNW, kSplitN, kPre>(s.hb, s.ld_hb, H, nullptr, 0, 0, bw.Wp, bw.Wp_s, bw.pinv, 2 * M,
+      node_gemm<NT, kNW, kSplitN, kPre, Geo<NF, NT, P>::kNodePFA>(s.hb, s.ld_hb, H, nullptr, 0, 0, bw.Wp, bw.Wp_s, bw.pinv, 2 * M,
                                         kPu ? bw.bp_u : bw.bp, 2 * M, false, nullptr, 0, s.P, s.ld_P, RP, nvalid, wave,
                                         lane, &pre);
       wg_sync<HALF>();
@@ -2438,7 +2448,7 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
     float* Q0 = s.P;
     float* Q1 = s.P + (kSplitN ? M + 4 : M + 1);   // 16-B aligned rows for the split node GEMMs
     constexpr bool kHu = kSplitG || Geo<NF, NT, P>::kL2T;   // log2-domain messages, scale in phi_h.0
-    node_gemm<NT, kNW, kSplitN, kPre>(s.macc, s.ld_m, M, s.hb, s.ld_hb, H, bw.Wh[0], kHu ? bw.Wh_s[0] : bw.Wh_sn0,
+    node_gemm<NT, kNW, kSplitN, kPre, Geo<NF, NT, P>::kNodePFA>(s.macc, s.ld_m, M, s.hb, s.ld_hb, H, bw.Wh[0], kHu ? bw.Wh_s[0] : bw.Wh_sn0,
                                       kHu ? bw.hinv[0] : bw.hinv_n0, M, bw.bh[0], M, true, nullptr, 0, Q0, s.ld_P, RP,
                                       nvalid, wave, lane, &pre);
     if constexpr (kPre) node_prefetch<kNW>(bw.Wh_s[1], M, 0, L == 1 ? H : M, RP, wave, lane, pre);
@@ -2450,13 +2460,13 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
       }
     }
     for (int l = 1; l < L; ++l) {
-      node_gemm<NT, kNW, kSplitN, kPre>(Q0, s.ld_P, M, nullptr, 0, 0, bw.Wh[l], bw.Wh_s[l], bw.hinv[l], M, bw.bh[l], M,
+      node_gemm<NT, kNW, kSplitN, kPre, Geo<NF, NT, P>::kNodePFA>(Q0, s.ld_P, M, nullptr, 0, 0, bw.Wh[l], bw.Wh_s[l], bw.hinv[l], M, bw.bh[l], M,
                                         true, nullptr, 0, Q1, s.ld_P, RP, nvalid, wave, lane, &pre);
       if constexpr (kPre) node_prefetch<kNW>(bw.Wh_s[l + 1], M, 0, l + 1 == L ? H : M, RP, wave, lane, pre);
       wg_sync<HALF>();
       float* tq = Q0; Q0 = Q1; Q1 = tq;
     }
-    node_gemm<NT, kNW, kSplitN, kPre>(Q0, s.ld_P, M, nullptr, 0, 0, bw.Wh[L], bw.Wh_s[L], bw.hinv[L], H, bw.bh[L], H,
+    node_gemm<NT, kNW, kSplitN, kPre, Geo<NF, NT, P>::kNodePFA>(Q0, s.ld_P, M, nullptr, 0, 0, bw.Wh[L], bw.Wh_s[L], bw.hinv[L], H, bw.bh[L], H,
                                       false, s.hb, s.ld_hb, s.hin, s.ld_hin, RP, nvalid, wave, lane, &pre);
     wg_sync<HALF>();
     STAMP(s, kStPhiH);

@@ -13,3 +13,7 @@ ECNF_STAMPS_LIB=tools/libecnf_hip_stamps_aldp.so timeout -k 10 120 python -u too
 cat gpurun_out/r4k/stamps_qm9_cols.json gpurun_out/r4k/stamps_qm9_g7.json | grep -v amdgpu.ids; \
 timeout -k 10 200 python -u tools/team_probe.py qm9 1 > gpurun_out/r4k/team_qm9.log 2>&1; tail -c 1200 gpurun_out/r4k/team_qm9.log; \
 bash tools/pmc_issue.sh r4k; tail -3 gpurun_out/prof_r4k/issue.log
+TV_GLOB='libt_[bn]*.so' timeout -k 10 200 python -u tools/time_variants.py 4 > gpurun_out/r4k/ab_pk_lj13.log 2>&1; tail -2 gpurun_out/r4k/ab_pk_lj13.log; \
+TV_CASE=qm9 TV_GLOB='libt_q*.so' timeout -k 10 240 python -u tools/time_variants.py 3 > gpurun_out/r4k/ab_pfa_qm9.log 2>&1; tail -2 gpurun_out/r4k/ab_pfa_qm9.log; \
+ECNF_LIB=tools/libt_q6.so timeout -k 10 150 python -u tools/team_probe.py qm9 1 > gpurun_out/r4k/team_q6.log 2>&1; tail -c 600 gpurun_out/r4k/team_q6.log; \
+ECNF_LIB=tools/libt_q2.so timeout -k 10 150 python -u tools/team_probe.py qm9 1 > gpurun_out/r4k/team_q2.log 2>&1; tail -c 600 gpurun_out/r4k/team_q2.log
