@@ -2093,19 +2093,41 @@ __device__ __forceinline__ void team_exchange(const Net& net, const Lds& s, cons
   auto ld16 = [&](int member, int fo) {
     return *reinterpret_cast<const f32x4*>(slot0 + (size_t)member * tm.p.slot + fo);
   };
-  for (int idx = tid; idx < N * M4; idx += NTHR) {
-    const int i = idx / M4, c = (idx - i * M4) * 4;
-    const int o0 = first_tile(i) % G, o1 = last_tile(i) % G;
-    f32x4 v = ld16(o0, i * M + c);
-    // atomically accumulated parts (no cross rows): 0 + a + b, whichever member holds each (exact in any order)
-    if (!net.cross && o1 != o0) v += ld16(o1, i * M + c);
-    *reinterpret_cast<f32x4*>(s.macc + i * s.ld_m + c) = v;
-  }
-  if (net.cross)
-    for (int idx = tid; idx < tpm * M4; idx += NTHR) {
-      const int t = idx / M4, c = (idx - t * M4) * 4;
-      *reinterpret_cast<f32x4*>(s.cross + t * s.ld_m + c) = ld16(t % G, off_x + t * M + c);
+  // message rows (items 0 .. nmsg - 1: receiver i, 4 columns), then the crossing continuation rows (tile t, 4
+  // columns), in batches of kB items per thread whose loads are all issued before their LDS stores: the slots were
+  // written through by other XCDs' workgroups, so every load is a memory round trip, and one per loop trip
+  // serialised ~14 of them per exchange
+  constexpr int kB = 8;
+  const int nmsg = N * M4, ntot = nmsg + (net.cross ? tpm * M4 : 0);
+  for (int base = tid; base < ntot; base += kB * NTHR) {
+    f32x4 v[kB];
+#pragma unroll
+    for (int u = 0; u < kB; ++u) {
+      const int idx = base + u * NTHR;
+      v[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (idx < nmsg) {
+        const int i = idx / M4, c = (idx - i * M4) * 4;
+        const int o0 = first_tile(i) % G, o1 = last_tile(i) % G;
+        v[u] = ld16(o0, i * M + c);
+        // atomically accumulated parts (no cross rows): 0 + a + b, whichever member holds each (exact in any order)
+        if (!net.cross && o1 != o0) v[u] += ld16(o1, i * M + c);
+      } else if (idx < ntot) {
+        const int t = (idx - nmsg) / M4, c = (idx - nmsg - t * M4) * 4;
+        v[u] = ld16(t % G, off_x + t * M + c);
+      }
     }
+#pragma unroll
+    for (int u = 0; u < kB; ++u) {
+      const int idx = base + u * NTHR;
+      if (idx < nmsg) {
+        const int i = idx / M4, c = (idx - i * M4) * 4;
+        *reinterpret_cast<f32x4*>(s.macc + i * s.ld_m + c) = v[u];
+      } else if (idx < ntot) {
+        const int t = (idx - nmsg) / M4, c = (idx - nmsg - t * M4) * 4;
+        *reinterpret_cast<f32x4*>(s.cross + t * s.ld_m + c) = v[u];
+      }
+    }
+  }
   for (int idx = tid; idx < N * D; idx += NTHR) {
     const int i = idx / D;
     const int o0 = first_tile(i) % G, o1 = last_tile(i) % G;

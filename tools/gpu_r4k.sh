@@ -17,3 +17,4 @@ TV_GLOB='libt_[bn]*.so' timeout -k 10 200 python -u tools/time_variants.py 4 > g
 TV_CASE=qm9 TV_GLOB='libt_q*.so' timeout -k 10 240 python -u tools/time_variants.py 3 > gpurun_out/r4k/ab_pfa_qm9.log 2>&1; tail -2 gpurun_out/r4k/ab_pfa_qm9.log; \
 ECNF_LIB=tools/libt_q6.so timeout -k 10 150 python -u tools/team_probe.py qm9 1 > gpurun_out/r4k/team_q6.log 2>&1; tail -c 600 gpurun_out/r4k/team_q6.log; \
 ECNF_LIB=tools/libt_q2.so timeout -k 10 150 python -u tools/team_probe.py qm9 1 > gpurun_out/r4k/team_q2.log 2>&1; tail -c 600 gpurun_out/r4k/team_q2.log
+ECNF_LIB=tools/libt_qx.so timeout -k 10 150 python -u tools/team_probe.py qm9 1 > gpurun_out/r4k/team_qx.log 2>&1; tail -c 600 gpurun_out/r4k/team_qx.log
