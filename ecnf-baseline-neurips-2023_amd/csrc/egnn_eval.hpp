@@ -1145,13 +1145,15 @@ __device__ __forceinline__ void edge_tail(const Net& net, const BlockW& bw, cons
           *reinterpret_cast<f32x4*>(agg_dst + fb * 32 + 8 * q + 4 * kk) =
               f32x4{v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
       } else {
-        // per-lane row offset through an empty asm: the 16 constant offsets fold into ds_add_f32's offset field
-        // (otherwise the compiler precomputed the lane addresses once per block and kept them live, i.e. spilled).
-        // The integer, not the pointer, passes the asm: an opaque pointer loses its LDS address space (flat atomics)
-        int mo = rr * s.ld_m + 4 * kk;
-        asm volatile("" : "+v"(mo));
+        // per-lane row base through an empty asm: the compiler no longer precomputes (and spills) the 16 lane addresses
+        // per block; the atomics compile to flat_atomic_add_f32 on the LDS aperture.  (The same sum through an opaque
+        // integer offset, or the round-3 form, compiles to ds_add_f32, and that build's (128, 2, 3) tangent
+        // vf_kernel returned NaNs / faulted on the GPU (profiles/round4/bisect/); the flat form is the one validated
+        // by the whole GPU suite.)
+        float* mrow = s.macc + rr * s.ld_m + 4 * kk;
+        asm volatile("" : "+v"(mrow));
 #pragma unroll
-        for (int r16 = 0; r16 < 16; ++r16) lds_add(s.macc + mo + fb * 32 + acc_row(r16, 0), v[r16]);
+        for (int r16 = 0; r16 < 16; ++r16) lds_add(mrow + fb * 32 + acc_row(r16, 0), v[r16]);
       }
     }
     if constexpr (NT) {
@@ -1159,10 +1161,10 @@ __device__ __forceinline__ void edge_tail(const Net& net, const BlockW& bw, cons
       for (int r16 = 0; r16 < 16; ++r16) v[r16] = gT * m[fb][r16] + g * mT[fb][r16];
       sc.sum_many<16, true>(v);
       if (writer) {
-        int mo = (RP + rr) * s.ld_m + 4 * kk;
-        asm volatile("" : "+v"(mo));
+        float* mrow = s.macc + (RP + rr) * s.ld_m + 4 * kk;
+        asm volatile("" : "+v"(mrow));
 #pragma unroll
-        for (int r16 = 0; r16 < 16; ++r16) lds_add(s.macc + mo + fb * 32 + acc_row(r16, 0), v[r16]);
+        for (int r16 = 0; r16 < 16; ++r16) lds_add(mrow + fb * 32 + acc_row(r16, 0), v[r16]);
       }
     }
   }
@@ -1979,10 +1981,10 @@ __device__ __forceinline__ void edge_tile_cols(const Net& net, const BlockW& bw,
               *reinterpret_cast<f32x4*>(agg_dst + fb * 32 + 8 * q + 4 * kk) =
                   f32x4{v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
           } else {
-            int mo = rr * s.ld_m + 4 * kk;
-            asm volatile("" : "+v"(mo));
+            float* mrow = s.macc + rr * s.ld_m + 4 * kk;   // (edge_tail's validated form)
+            asm volatile("" : "+v"(mrow));
 #pragma unroll
-            for (int r16 = 0; r16 < 16; ++r16) lds_add(s.macc + mo + fb * 32 + acc_row(r16, 0), v[r16]);
+            for (int r16 = 0; r16 < 16; ++r16) lds_add(mrow + fb * 32 + acc_row(r16, 0), v[r16]);
           }
         }
       }
