@@ -28,7 +28,8 @@ for B in batches:
     steps = 20
     rows = {}
     ref = None
-    for mode in (1, 0, 2, 4, 7, 13):   # 1: batch path, 0: auto (QM9 B <= 9: column-split, G = 26), >= 2: tile-dealt
+    modes = [int(m) for m in os.environ.get("TP_MODES", "1,0,2,4,7,13").split(",")]
+    for mode in modes:   # 1: batch path, 0: auto (QM9 B <= 9: column-split, G = 26), >= 2: tile-dealt
         h.set_team(mode)
         G = h.team_workgroups(B)
         key = f"{'auto' if mode == 0 else 'forced'}_G{G}"
