@@ -1913,6 +1913,9 @@ __device__ __forceinline__ void edge_tile_cols(const Net& net, const BlockW& bw,
   const float length = sqrtf(zero ? 1.0f : x2);
   const float len2 = length * length;
   float* xs = lds_xs(net, s);
+#ifdef ECNF_STAMPS   // diagnostic build: wave 0's sub-phases (the edge stamp slots of edge_tile)
+  unsigned long long t_sub = __builtin_amdgcn_s_memtime();
+#endif
   // phi_e layer 1 from the per-node halves for this wave's blocks (egnn.py:76,79): u = P_s[s] + P_r[r] + |r|^2 w_d'
   {
     const float* Ps = s.P + rs * s.ld_P;
@@ -1949,7 +1952,9 @@ __device__ __forceinline__ void edge_tile_cols(const Net& net, const BlockW& bw,
   xs_load<NF>(xs, X, lane);
   f32x16 m[NF];
   // phi_e layers 2..L
+  STAMP_LANE0(s, kStEdgeLayer1, t_sub);
   cols_segment<NF, L - 1>(X, m, launder_uniform(bw.Ws), s.vecs, xs, wave, lane);
+  STAMP_LANE0(s, kStEdgeChainE, t_sub);
   SegScan sc;
   sc.init(valid ? rr : -1, li);
   const bool writer = valid && sc.tail;
@@ -1998,11 +2003,14 @@ __device__ __forceinline__ void edge_tile_cols(const Net& net, const BlockW& bw,
       put_pair<NF, fb, 2 * k>(X, m[fb][2 * k], m[fb][2 * k + 1]);
     });
   });
+  STAMP_LANE0(s, kStEdgeAgg, t_sub);
   cols_segment<NF, L>(X, m, launder_uniform(bw.Ws + (size_t)(L - 1) * SplitPlan<NF, 1>::GL * kPieces * 256),
                       s.vecs + (L - 1) * NF * 32, xs, wave, lane);
   // phi_x output Dense(1) and the shifts (egnn.py:83-94): every wave computes them, wave 0 stores
+  STAMP_LANE0(s, kStEdgePhiX, t_sub);
   edge_shift<NF, 0, L, D>(net, bw, s, m, m, writer, sc, rr, r, dr, length, 0.f, lane, wave == 0);
   __syncthreads();   // the image is rewritten by the next tile's layer 1
+  STAMP_LANE0(s, kStEdgeTail, t_sub);
 }
 
 // ---------------------------------------------------------------------------------------------------
