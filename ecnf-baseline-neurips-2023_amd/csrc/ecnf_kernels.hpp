@@ -125,7 +125,7 @@ __device__ inline bool check_features(const Net& net, int* f) {
 template <int NF, int NT, int L, int D, int P, bool TEAM, bool HALF, bool COLS>
 __device__ __forceinline__ void joint_field(const Net& net, const Lds& s, const SolverLds& st, const SolveP& sp,
                                             float* kx_out, float* kl_out, const TeamCtx* tm, int* tepoch) {
-  constexpr int kThreads = HALF ? 256 : Geo<NF, NT, P>::NTHR;
+  constexpr int kThreads = HALF ? 256 : kernel_threads<NF, NT, P, COLS>();
   // per-thread indices are re-derived (opaque_tid) on each side of the evaluation: kept live across it, they spill
   const int MPW = solver_size(0), ND = solver_size(1);
   int tid = vtid<HALF>();
@@ -192,14 +192,14 @@ enum Phase { kEuler = 0, kInit0 = 1, kInit1 = 2, kFsal = 3, kStage = 4 };
 // The whole solve as a phase machine around ONE field evaluation per loop trip.  TEAM: the team (latency) mode
 // instantiation (egnn_eval.hpp team_exchange; launched only with sp.team.G > 1, compiled for team_shape)
 template <int NF, int NT, int L, int D, int P, bool TEAM = false, bool HALF = false, bool COLS = false>
-__global__ __launch_bounds__((HALF ? 512 : Geo<NF, NT, P>::NTHR)) __attribute__((amdgpu_waves_per_eu(Geo<NF, NT, P>::WPE))) void integrate_kernel(Net net, SolveP sp, const float* __restrict__ y0,
+__global__ __launch_bounds__((HALF ? 512 : kernel_threads<NF, NT, P, COLS>())) __attribute__((amdgpu_waves_per_eu(Geo<NF, NT, P>::WPE))) void integrate_kernel(Net net, SolveP sp, const float* __restrict__ y0,
                                                                   const int32_t* __restrict__ feat,
                                                                   const float* __restrict__ eps, float* y1,
                                                                   float* dlogp, int32_t* nfe_out,
                                                                   int32_t* status_out, int B) {
   // HALF (halves mode, egnn_eval.hpp wg_sync): two independent 256-thread halves, half h = threadIdx.x / 256 with
   // its own net.lds_floats of LDS and molecules [(2 blockIdx + h) MPW, +MPW)
-  constexpr int kThreads = HALF ? 256 : Geo<NF, NT, P>::NTHR;
+  constexpr int kThreads = HALF ? 256 : kernel_threads<NF, NT, P, COLS>();
   extern __shared__ float smem_all[];
   const int half = HALF ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 8)) : 0;
   if constexpr (HALF) {
@@ -596,8 +596,8 @@ hipError_t launch_integrate(const Net& net, size_t lds, const SolveP& sp, const 
     const float* a_eps = eps;
     int a_B = B;
     void* args[] = {&n, &p, &a_y0, &a_feat, &a_eps, &y1, &dlogp, &nfe, &status, &a_B};
-    return hipLaunchCooperativeKernel((const void*)kt, dim3(B * sp.team.G), dim3(Geo<NF, NT, P>::NTHR), args, lds,
-                                      stream);
+    const int nthr = sp.team.cols ? kernel_threads<NF, NT, P, true>() : Geo<NF, NT, P>::NTHR;
+    return hipLaunchCooperativeKernel((const void*)kt, dim3(B * sp.team.G), dim3(nthr), args, lds, stream);
     }
   }
   if (sp.team.G > 1) return hipErrorInvalidValue;   // no team kernel for this shape (team_size never asks for one)

@@ -103,6 +103,13 @@ struct Geo {
 #ifndef ECNF_SPLIT_NW
 #define ECNF_SPLIT_NW 8
 #endif
+#ifndef ECNF_COLS_NW
+// waves of the column-split team kernel (M = 256 split primal): 8, one output block of each chain layer per wave, two
+// waves per SIMD to hide the fragment stream (QM9 B = 1 Euler-20: 456 -> 311 us per evaluation, bitwise equal;
+// profiles/round4/r4q).  The batch-path and tile-dealt M = 256 kernels stay at 4 waves: at 8 they spill 828 B per
+// lane (2283 -> 2587 us per evaluation).
+#define ECNF_COLS_NW 8
+#endif
 #ifndef ECNF_TAN_NW_NF2
 #define ECNF_TAN_NW_NF2 8
 #endif
@@ -124,6 +131,11 @@ struct Geo {
   // them) run a deeper ring than the 256-register kernels
   static constexpr int kNodePFA = (kSplit && NF == 8) ? ECNF_NODE_PFA_WIDE : ECNF_NODE_PFA;
 };
+// waves / threads per workgroup of a kernel: Geo's, or ECNF_COLS_NW for the column-split team kernel
+template <int NF, int NT, int P, bool COLS>
+constexpr int kernel_waves() { return COLS ? ECNF_COLS_NW : Geo<NF, NT, P>::NW; }
+template <int NF, int NT, int P, bool COLS>
+constexpr int kernel_threads() { return 64 * kernel_waves<NF, NT, P, COLS>(); }
 constexpr int kMaxBlocks = 10;
 constexpr int kMaxPhiH = 5;     // L + 1 <= 5
 constexpr int kMaxHalfT = 8;    // T <= 16
@@ -1715,9 +1727,9 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
 }
 
 // ---------------------------------------------------------------------------------------------------
-// Column-split team mode (team cols; the M = 256 split primal kernels, 4 waves): every member workgroup of a
-// molecule's team runs ONE edge tile per block, and its waves split each chain layer of that tile by output block
-// (wave w: blocks [w NJ, (w + 1) NJ), NJ = NF / 4), exchanging the layer through an LDS image (Lds::xs): split pieces
+// Column-split team mode (team cols; the M = 256 split primal kernels, ECNF_COLS_NW = 8 waves): every member
+// workgroup of a molecule's team runs ONE edge tile per block, and its waves split each chain layer of that tile by
+// output block (wave w: blocks [w NJ, (w + 1) NJ), NJ = NF / ECNF_COLS_NW), exchanging the layer through an LDS image (Lds::xs): split pieces
 // in the MFMA B-operand layout between layers, fp32 after a segment's last layer.  Per output element the arithmetic
 // is chain_split's (the same MFMA sequence from the bias column, the same log2-domain SiLU, pair split and fp32 last
 // layer), and the gate / phi_x-output dot products read the whole fp32 layer back and sum in the batch order
@@ -1820,7 +1832,7 @@ __device__ __forceinline__ void cols_act(f32x16 (&acc)[NJ], float* xs, int j0, i
 template <int NF, int NL>
 __device__ __forceinline__ void cols_segment(SplitX<NF>& X, f32x16 (&m)[NF], const unsigned* __restrict__ W,
                                              const float* bias, float* xs, int wave, int lane) {
-  constexpr int NJ = NF / 4, GB = 2 * NF, GL = GB * NF, NG = NJ * GB, NQ = NL * NG, PF = ECNF_COLS_PF;
+  constexpr int NJ = NF / ECNF_COLS_NW, GB = 2 * NF, GL = GB * NF, NG = NJ * GB, NQ = NL * NG, PF = ECNF_COLS_PF;
   const int j0 = wave * NJ, kk = lane >> 5;
   const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned*>(W), (short)0,
                                                                          0x7fffffff, 0x00020000);
@@ -1883,8 +1895,8 @@ __device__ __forceinline__ void cols_segment(SplitX<NF>& X, f32x16 (&m)[NF], con
 template <int NF, int L, int D>
 __device__ __forceinline__ void edge_tile_cols(const Net& net, const BlockW& bw, const Lds& s, int tile, int wave,
                                                int lane, bool agg) {
-  static_assert(NF % 4 == 0, "cols mode deals the output blocks over 4 waves");
-  constexpr int NJ = NF / 4, M = NF * 32;
+  static_assert(NF % ECNF_COLS_NW == 0, "cols mode deals the output blocks over the workgroup's waves");
+  constexpr int NJ = NF / ECNF_COLS_NW, M = NF * 32;
   const int kk = lane >> 5, li = lane & 31, j0 = wave * NJ;
   const int N = net.N, nn1 = N - 1;
   const int mol = (tile * 32) / net.EP;
@@ -2157,7 +2169,7 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
                           float* v_out, float* tan_out, const int* act = nullptr, int sparse_a = -1,
                           float* pcache = nullptr, int pmode = 0, const TeamCtx* tm = nullptr,
                           int* tepoch = nullptr) {
-  constexpr int kNW = HALF ? 4 : Geo<NF, NT, P>::NW, kNT = HALF ? 256 : Geo<NF, NT, P>::NTHR;
+  constexpr int kNW = HALF ? 4 : kernel_waves<NF, NT, P, COLS>(), kNT = HALF ? 256 : kernel_threads<NF, NT, P, COLS>();
   constexpr bool kSplitG = Geo<NF, NT, P>::kSplit;
   constexpr bool kSplitN = Geo<NF, NT, P>::kSplitN;   // split node GEMMs (primal split kernels and tangent kernels)
 #ifndef ECNF_NODE_PREFETCH

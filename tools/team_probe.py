@@ -47,6 +47,9 @@ for B in batches:
             ts.append(a.elapsed_time(b))
         ms = sorted(ts)[2]
         rows[key] = {"kernel_ms": ms, "us_per_eval": 1e3 * ms / steps, "bitwise_vs_batch": bool(torch.equal(y, ref))}
+    if os.environ.get("TP_DUMP"):   # the batch-path (or first mode's) sample, for cross-library comparison
+        import numpy as np
+        np.save(f"{os.environ['TP_DUMP']}_B{B}.npy", ref.cpu().numpy())
     h.set_team(0)
     # the reference timer's call: PID, one molecule, host copy
     walls, nfes = [], []
