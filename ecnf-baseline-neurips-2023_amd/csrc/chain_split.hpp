@@ -2,22 +2,20 @@
 //
 // Why: on gfx950 v_mfma_f32_32x32x2_f32 runs at the fp32 VECTOR rate and shares the SIMD's vector issue, so every
 // SiLU / scan instruction of the fp32-MFMA chain adds to its time (measured: tools/micro/chain_bench.hip).  The
-// 16-bit MFMAs (v_mfma_f32_32x32x16_{f16,bf16}, 32 cycles for 16x the fp32 MFMA's k-depth) run on the matrix cores
-// and leave 24 of their 32 cycles of vector issue free.
+// 16-bit MFMAs (v_mfma_f32_32x32x16_f16, 32 cycles for 16x the fp32 MFMA's k-depth) run on the matrix cores and
+// leave 24 of their 32 cycles of vector issue free.
 //
-// Accuracy (default, fp16 pieces): every fp32 operand x is split into two fp16 values by round-to-nearest,
-// x = x0 + x1, |x - x0| <= 2^-11 |x|, and x1 = fp16(x - x0) carries the rest to 2^-22 |x| (one v_cvt_pk_f16_f32
-// and two v_fma_mix per pair of values).  A product keeps the three cross terms w1x0, w0x1, w0x0 (smallest first)
-// and accumulates them in fp32 inside the MFMA; the dropped w1x1 and the piece roundings are <= 2^-21 |w x|.
-// Node-GEMM weights are split on the host after scaling each matrix by a power of two s (max |w s| in
-// [2^12, 2^13)), so both weight pieces are normal fp16 numbers; their epilogue multiplies the accumulator by 1/s
-// (exact) in the FMA that adds the bias.  Edge-chain weights (ECNF_CHAIN_BIAS_INIT, the default) are split
-// unscaled and every output block's accumulator starts at its bias column, so the activation needs no FMA (-1 VALU
-// per element; LJ13 26.70 -> 26.01 ms); the host refuses |w| >= 2^15.  Activations and unscaled weights keep
-// their pieces' absolute error <= 2^-25 below 2^-14 (fp16 subnormals): per dot product of K = 128 terms that is
-// <= 128 * 2^-25 * max|x| absolute, i.e. ~1e-6 relative for O(0.1) weights.
-// -DECNF_SPLIT_BF16 builds the earlier form: three bf16 pieces (x0 + x1 + x2, |x2| <= 2^-17 |x|), six cross terms
-// (w2x0, w1x1, w0x2, w1x0, w0x1, w0x0), no scaling (bf16 has fp32's exponent range).
+// Accuracy: every fp32 operand x is split into two fp16 values by round-to-nearest, x = x0 + x1,
+// |x - x0| <= 2^-11 |x|, and x1 = fp16(x - x0) carries the rest to 2^-22 |x| (one v_cvt_pk_f16_f32 and two v_fma_mix
+// per pair of values).  A product keeps the three cross terms w1x0, w0x1, w0x0 (smallest first) and accumulates them
+// in fp32 inside the MFMA; the dropped w1x1 and the piece roundings are <= 2^-21 |w x|.  Node-GEMM weights are split
+// on the host after scaling each matrix by a power of two s (max |w s| in [2^12, 2^13)), so both weight pieces are
+// normal fp16 numbers; their epilogue multiplies the accumulator by 1/s (exact) in the FMA that adds the bias.
+// Edge-chain weights are split unscaled and every output block's accumulator starts at its bias column, so the
+// activation needs no FMA (-1 VALU per element; LJ13 26.70 -> 26.01 ms); the host refuses |w| >= 2^15.  Activations
+// and unscaled weights keep their pieces' absolute error <= 2^-25 below 2^-14 (fp16 subnormals): per dot product of
+// K = 128 terms that is <= 128 * 2^-25 * max|x| absolute, i.e. ~1e-6 relative for O(0.1) weights.  (The round-1 form,
+// three bf16 pieces and six cross terms, ran LJ13 in 56.8 ms against 36.5 ms for the fp16 pair.)
 //
 // Layout: one 32-edge tile per wave, features on MFMA rows, edges on lanes (as the fp32 chain).  A k-step of
 // 16 input features of block fb is accumulator registers 8u..8u+7 (u = 0, 1): lane (c, h) holds features
@@ -32,32 +30,17 @@
 #pragma once
 // (included by egnn_eval.hpp inside namespace ecnf)
 
-#ifndef ECNF_CHAIN_BIAS_EPILOGUE   // -DECNF_CHAIN_BIAS_EPILOGUE: the scaled-weight form (bias + 1/s in stage A)
-#define ECNF_CHAIN_BIAS_INIT 1
-#endif
-
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef const ECNF_GLOBAL u32x4* gu32x4_p;
 
-#ifdef ECNF_SPLIT_BF16
-constexpr int kPieces = 3;
-constexpr int kTerms = 6;
-#else
 constexpr int kPieces = 2;
 constexpr int kTerms = 3;
-#endif
-// cross term t: (weight piece, activation piece), smallest first
-__host__ __device__ constexpr int term_w(int t) {
-  return kPieces == 3 ? (t == 0 ? 2 : (t == 1 || t == 3) ? 1 : 0) : (t == 0 ? 1 : 0);
-}
-__host__ __device__ constexpr int term_x(int t) {
-  return kPieces == 3 ? (t == 2 ? 2 : (t == 1 || t == 4) ? 1 : 0) : (t == 1 ? 1 : 0);
-}
+// cross term t: (weight piece, activation piece), smallest first: w1 x0, w0 x1, w0 x0
+__host__ __device__ constexpr int term_w(int t) { return t == 0 ? 1 : 0; }
+__host__ __device__ constexpr int term_x(int t) { return t == 1 ? 1 : 0; }
 // bytes of one split group / k-step fragment set: kPieces x 64 lanes x 16 B
 constexpr int kPieceBytes = 1024;
 constexpr int kGroupU32 = kPieces * 256;
@@ -69,34 +52,13 @@ struct SplitX {
 };
 
 __device__ __forceinline__ f32x16 mfma_split(u32x4 a, u32x4 b, const f32x16& c) {
-#ifdef ECNF_SPLIT_BF16
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0,
-                                                 0, 0);
-#else
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0,
                                                 0, 0);
-#endif
 }
 
 // y0, y1 -> kPieces packed 16-bit pairs (RNE), y = sum of the pieces per element
 __device__ __forceinline__ void split_pair(float y0, float y1, unsigned (&p)[kPieces]) {
-#ifdef ECNF_SPLIT_BF16
-  p[0] = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){y0, y1}, bf16x2));
-  float r0 = y0 - __builtin_bit_cast(float, p[0] << 16);
-  float r1 = y1 - __builtin_bit_cast(float, p[0] & 0xffff0000u);
-  p[1] = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){r0, r1}, bf16x2));
-  r0 -= __builtin_bit_cast(float, p[1] << 16);
-  r1 -= __builtin_bit_cast(float, p[1] & 0xffff0000u);
-  p[2] = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){r0, r1}, bf16x2));
-#else
   p[0] = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){y0, y1}, f16x2));
-#ifdef ECNF_SPLIT_C_RESIDUAL   // experiment: the residual in plain C (schedulable VALU, 2 more instructions per pair)
-  {
-    const f16x2 h = __builtin_bit_cast(f16x2, p[0]);
-    p[1] = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){y0 - (float)h[0], y1 - (float)h[1]}, f16x2));
-    return;
-  }
-#endif
   // p1 = fp16(y - fp16 piece 0) per half: the mixed-precision FMA reads the f16 half directly, the difference is
   // exact in fp32 and rounded once (hipcc does not form v_fma_mix from C here)
   unsigned lo;
@@ -105,7 +67,6 @@ __device__ __forceinline__ void split_pair(float y0, float y1, unsigned (&p)[kPi
       : "=&v"(lo)
       : "v"(p[0]), "v"(y0), "v"(y1));
   p[1] = lo;
-#endif
 }
 
 // SiLU in the log2 domain.  The split kernels carry every pre-activation as u = -log2(e) t (the host folds the
@@ -131,8 +92,8 @@ __device__ __forceinline__ void put_pair(SplitX<NF>& X, float y0, float y1) {
 
 // The activation of a layer's output block runs as a 3-stage software pipeline across MFMA groups, so the VALU that
 // fills each MFMA gap has no dependency on the VALU of the same gap (no transcendental-latency stalls):
-//   stage A (group gA): u = acc inv + b'; e = 2^u          (v_fma, v_exp)
-//   stage B (group gB): r = 1 / (1 + e)                      (v_add, v_rcp)
+//   stage A (group gA): u = acc (+ the bias and 1/s for 3-piece weights); e = 2^u   (v_exp)
+//   stage B (group gB): r = 1 / (1 + e)                                              (v_add, v_rcp)
 //   stage C (group gC): y' = u r, split into the next layer's input buffer (v_mul, v_cvt_pk, 2 v_fma_mix), or kept
 //                       fp32 in place in acc for the segment's last layer
 // An item is one pair of elements (rows 2p, 2p+1 of the accumulator registers) of output block j of layer l.
@@ -204,29 +165,12 @@ struct ChainInv {
   float v[2 * 4 - 1];
 };
 
-#ifndef ECNF_CHAIN_PRIO
-#define ECNF_CHAIN_PRIO 1   // wave priority inside chain_split (s_setprio)
-#endif
-#ifndef ECNF_SPLIT_PF
-#define ECNF_SPLIT_PF 3
-#endif
-#ifndef ECNF_SPLIT_PF3   // weight groups in flight for the 3-piece (exact-weight) chains
-#define ECNF_SPLIT_PF3 3
-#endif
-#ifndef ECNF_SPLIT_PF3_NARROW   // ... at M = 64, where the kernel runs 2 waves per SIMD (ALDP A/B: 50.5 -> 50.2 ms)
-#define ECNF_SPLIT_PF3_NARROW 2
-#endif
-// the activation's stage-B add and stage-C multiply as packed fp32 (v_pk_add_f32 / v_pk_mul_f32) where the compiler
-// keeps the pair in an aligned register pair (bit-identical; LJ13 27.14 -> 27.02 ms A/B, profiles/round2/e3);
-// -DECNF_SPLIT_NO_PK: scalar
-#if !defined(ECNF_SPLIT_NO_PK) && !defined(ECNF_SPLIT_PK)
-#define ECNF_SPLIT_PK 1
-#endif
+constexpr int kChainPrio = 1;        // wave priority inside the chain (s_setprio; 2 or 3: no further change)
+constexpr int kSplitPF = 3;          // weight groups in flight ahead of the MFMAs (PF 2 ... 10: no difference)
+constexpr int kSplitPF3 = 3;         // ... for the 3-piece (exact-weight) chains (2 / 3 equal; 5 spilled 119 registers)
+constexpr int kSplitPF3Narrow = 2;   // ... at M = 64, where the kernel runs 2 waves per SIMD (ALDP 50.5 -> 50.2 ms)
 
 __device__ __forceinline__ u32x4 wload(__amdgpu_buffer_rsrc_t rsrc, int voff, int soff) {
-#ifdef ECNF_SPLIT_WLOAD_SAME   // timing experiment: every group reads the first group's fragments (L1-resident)
-  soff &= 2047;
-#endif
   return __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, soff, 0);
 }
 
@@ -239,49 +183,31 @@ __device__ __forceinline__ auto& pick(A& a, B& b) {
 // activations y' (log2 domain, silu_u) in fp32 (accumulator layout).  XA / XB are both clobbered.
 // Weights: packed split fragments [layer][group][piece][lane] (16 B), read as buffer loads with the group
 // offset in an SGPR, PF groups ahead; biases: LDS [NL][M] (log2 domain), each item's two (adjacent) rows read one
-// group before its stage A; inv.v[l]: 1 / the weight scale of layer l.
-#ifdef ECNF_SPLIT_WLDS
-__shared__ unsigned g_wlds_exp[8 * kPieces * 256];
-#endif
-#ifdef ECNF_SPLIT_RING
-// experiment: a workgroup-shared LDS ring of weight fragments.  Every wave runs the same chain in lockstep; the
-// segment's groups are streamed in intervals of RIV groups, double-buffered: during interval i each wave loads its
-// share of interval i + 1's pieces from global memory into registers and writes them to the other half at the end
-// of the interval, then a workgroup barrier publishes them.  One global fetch per piece per workgroup instead of
-// one per wave; the waves read the fragments from LDS (2 ds_read_b128 per group).
-#ifndef ECNF_RING_IV
-#define ECNF_RING_IV 4
-#endif
-constexpr int kRingIV = ECNF_RING_IV;
-__shared__ unsigned g_ring[2 * kRingIV * kPieces * 256];
-#endif
+// group before its stage A; inv.v[l]: 1 / the weight scale of layer l (3-piece weights).
 // NT = 1 (forward-mode tangent, the divergence kernels): XAT / XBT / accT carry the tangent of every activation
 // through the same layers.  Each weight fragment feeds 2 kTerms MFMAs (primal and tangent interleaved); the
 // tangent of a layer is du = accT inv (no bias) and dy' = silu'(t) du = r (1 - ln2 u (1 - r)) du with the primal's
 // r = 1 / (1 + 2^u) (silu'(t) = sigma(t) (1 + t (1 - sigma(t))), t = -ln2 u).
 // WP: weight pieces per fragment group.  kPieces (2): the primal kernels' unscaled pieces, accumulators started at
-// the bias column (ECNF_CHAIN_BIAS_INIT).  3 (the divergence kernels, kWExact): the weights scaled by a power of two
-// per layer and split into three fp16 pieces w0 + w1 + w2 that hold the fp32 weight EXACTLY, the primal MFMAs adding
-// the fourth term w2 x0 (smallest first) and the activation applying 1/s and the bias in an FMA.  Two pieces represent
-// a weight only to 2^-22 (and unscaled small weights far worse, in fp16 subnormals): a FIXED perturbation of the
-// network, which the exact trace sums coherently over its N*D diagonal entries (LJ13: +1.2e-6 relative in tr J, 8x the
-// fp32 rounding error; tools/diag/trace_precision.py).  The tangent MFMAs keep three terms on pieces 0 and 1.
+// the bias column.  3 (the divergence kernels, kWExact): the weights scaled by a power of two per layer and split into
+// three fp16 pieces w0 + w1 + w2 that hold the fp32 weight EXACTLY, the primal MFMAs adding the fourth term w2 x0
+// (smallest first) and the activation applying 1/s and the bias in an FMA.  Two pieces represent a weight only to
+// 2^-22 (and unscaled small weights far worse, in fp16 subnormals): a FIXED perturbation of the network, which the
+// exact trace sums coherently over its N*D diagonal entries (LJ13: +1.2e-6 relative in tr J, 8x the fp32 rounding
+// error; tools/diag/trace_precision.py).  The tangent MFMAs keep three terms on pieces 0 and 1.
 template <int NF, int NL, int NT = 0, int WP = kPieces>
 __device__ __forceinline__ void chain_split(SplitX<NF>& XA, SplitX<NF>& XB, f32x16 (&acc)[NF],
                                             const unsigned* __restrict__ Wpk, const float* __restrict__ bias,
                                             const ChainInv& inv, int lane, SplitX<NF>& XAT, SplitX<NF>& XBT,
                                             f32x16 (&accT)[NF]) {
   using Plan = SplitPlan<NF, NL>;
-  static_assert(WP == kPieces || (WP == 3 && kPieces == 2), "3-piece weights extend the fp16 split");
-#ifdef ECNF_CHAIN_BIAS_INIT
-  constexpr bool kBI = WP == kPieces;
-#else
-  constexpr bool kBI = false;
-#endif
+  static_assert(WP == kPieces || WP == 3, "2-piece weights, or the exact 3-piece weights");
+  static_assert(NT == 0 || NT == 1, "primal, or primal + one tangent");
+  constexpr bool kBI = WP == kPieces;   // accumulators start at the bias column (unscaled weights)
   // the chain wave issues first on its SIMD while its partner wave is in VALU / LDS work (A/B: 26.14 -> 25.99 ms)
-  __builtin_amdgcn_s_setprio(ECNF_CHAIN_PRIO);
+  __builtin_amdgcn_s_setprio(kChainPrio);
   constexpr int GB = Plan::GB, GL = Plan::GL, G = Plan::G, NI = Plan::NI,
-                PF = WP == 3 ? (NF <= 2 ? ECNF_SPLIT_PF3_NARROW : ECNF_SPLIT_PF3) : ECNF_SPLIT_PF;
+                PF = WP == 3 ? (NF <= 2 ? kSplitPF3Narrow : kSplitPF3) : kSplitPF;
   constexpr int GE = Plan::last_group() + 1;   // groups including the VALU-only tail
   const int kk = lane >> 5;
   const float* lbias = bias + 4 * kk;
@@ -289,46 +215,12 @@ __device__ __forceinline__ void chain_split(SplitX<NF>& XA, SplitX<NF>& XB, f32x
                                                                          0x7fffffff, 0x00020000);
   const int voff = lane * 16;
   u32x4 wbuf[PF + 1][WP];
-#ifdef ECNF_SPLIT_RING
-  static_assert(WP == kPieces, "the ring experiment streams two pieces");
-  static_assert(G % kRingIV == 0, "segment groups must fill whole ring intervals");
-  const int rwave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), rnw = blockDim.x >> 6;
-  constexpr int kIvPieces = kRingIV * kPieces;
-  // this wave's pieces of an interval: q = rwave, rwave + rnw, ... (< kIvPieces); at most 2 per wave (rnw >= 4)
-  u32x4 rnext[2];
-  auto ring_fetch = [&](int iv) {
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int q = rwave + k * rnw;
-      if (q < kIvPieces) rnext[k] = wload(rsrc, voff, (iv * kIvPieces + q) * kPieceBytes);
-    }
-  };
-  auto ring_store = [&](int iv) {
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int q = rwave + k * rnw;
-      if (q < kIvPieces) *reinterpret_cast<u32x4*>(g_ring + (((iv & 1) * kIvPieces + q) * 256 + lane * 4)) = rnext[k];
-    }
-  };
-  auto ring_read = [&](int gg, u32x4 (&w)[kPieces]) {
-#pragma unroll
-    for (int p = 0; p < kPieces; ++p)
-      w[p] = *reinterpret_cast<const u32x4*>(g_ring + (((((gg / kRingIV) & 1) * kRingIV + gg % kRingIV) * kPieces + p) * 256 +
-                                                       lane * 4));
-  };
-  ring_fetch(0);
-  ring_store(0);
-  __syncthreads();
-  if (kRingIV < G) ring_fetch(1);
-  ring_read(0, wbuf[0]);
-#else
 #pragma unroll
   for (int gg = 0; gg < PF && gg < G; ++gg)
 #pragma unroll
     for (int p = 0; p < WP; ++p) wbuf[gg][p] = wload(rsrc, voff, (gg * WP + p) * kPieceBytes);
-#endif
   // per-item pipeline registers (SSA after unrolling: only live items occupy registers)
-  f32x2 bv[NI], uv[NI], ev[NI], dv[NI], e2v[NI];
+  f32x2 bv[NI], uv[NI], ev[NI], dv[NI];
   // kBI: each output block's accumulator starts at its (log2-domain) bias column and the weights are unscaled, so
   // stage A needs no FMA; a block's 16 biases (rows acc_row(r, kk)) are 4 x 16-B LDS reads, issued 2 groups ahead
   auto bias_block = [&](int off) {
@@ -356,28 +248,15 @@ __device__ __forceinline__ void chain_split(SplitX<NF>& XA, SplitX<NF>& XB, f32x
     constexpr int gg = decltype(GGc)::value;
     constexpr bool mfma_group = gg < G;
     constexpr int l = gg / GL, g = gg % GL, jb = g / GB, fb = (g % GB) >> 1, u = g & 1;
-    constexpr int nA = Plan::count(gg, 0), nB = Plan::count(gg, 1), nC = Plan::count(gg, 2);
     constexpr int nbias = kBI ? 0 : Plan::count(gg + 1, 0);
     constexpr int nxt = l * NF + jb + 1;   // the next output block of the segment
     constexpr bool load_cb = kBI && mfma_group && (g % GB) == GB - 2 && nxt < NL * NF;
     if constexpr (load_cb) cb = bias_block((nxt / NF) * NF * 32 + (nxt % NF) * 32);
-#if defined(ECNF_SPLIT_RING)
-    // next group's fragments from the ring, unless the next group opens a new interval (read after the barrier)
-    if constexpr (gg + 1 < G && (gg + 1) % kRingIV != 0) ring_read(gg + 1, wbuf[(gg + 1) % (PF + 1)]);
-#elif defined(ECNF_SPLIT_WLDS)   // timing experiment: fragments from an LDS image of 8 groups (g_wlds_exp)
-    if constexpr (gg + PF < G) {
-#pragma unroll
-      for (int p = 0; p < kPieces; ++p)
-        wbuf[(gg + PF) % (PF + 1)][p] =
-            *reinterpret_cast<const u32x4*>(g_wlds_exp + ((((gg + PF) & 7) * kPieces + p) * 256 + lane * 4));
-    }
-#elif !defined(ECNF_SPLIT_NO_WLOAD)   // NO_WLOAD timing experiment: reuse the first PF groups' weights
     if constexpr (gg + PF < G) {
 #pragma unroll
       for (int p = 0; p < WP; ++p)
         wbuf[(gg + PF) % (PF + 1)][p] = wload(rsrc, voff, ((gg + PF) * WP + p) * kPieceBytes);
     }
-#endif
     // biases of the next group's stage-A items
     static_for<nbias>([&](auto Kc) {
       constexpr int id = Plan::nth(gg + 1, 0, decltype(Kc)::value);
@@ -398,28 +277,15 @@ __device__ __forceinline__ void chain_split(SplitX<NF>& XA, SplitX<NF>& XB, f32x
         } else {
           acc[jb] = mfma_split(A[pa], B[pb], kBI ? cb : z);
         }
-        if constexpr (NT) accT[jb] = mfma_split(A[pa], BT[pb], (NT == 2 && kBI) ? cb : z);
+        if constexpr (NT) accT[jb] = mfma_split(A[pa], BT[pb], z);
       } else {
         if constexpr (WP == 3 && t == 0) acc[jb] = mfma_split(A[2], B[0], acc[jb]);
         acc[jb] = mfma_split(A[pa], B[pb], acc[jb]);
         if constexpr (NT) accT[jb] = mfma_split(A[pa], BT[pb], accT[jb]);
       }
     };
-#if defined(ECNF_SPLIT_CHEAP_ACT)   // timing experiment: keep the data flow (one VALU per pair), drop the arithmetic
-    static_for<nC>([&](auto Kc) {
-      constexpr int id = Plan::nth(gg, 2, decltype(Kc)::value);
-      constexpr typename Plan::Item it = Plan::item(id);
-      constexpr int r = 2 * it.p;
-      if constexpr (it.l < NL - 1) {
-        auto& Xo = pick<(it.l + 1) & 1>(XA, XB);
-        const unsigned q = __builtin_bit_cast(unsigned, acc[it.j][r]) ^ __builtin_bit_cast(unsigned, acc[it.j][r + 1]);
-        Xo.v[it.j][r >> 3][0][(r & 7) >> 1] = q;
-        Xo.v[it.j][r >> 3][1][(r & 7) >> 1] = q;   // every piece defined: no MFMA folds away
-      }
-    });
-#elif !defined(ECNF_SPLIT_NO_ACT)
     // stage A
-    auto stageA = [&]() { static_for<nA>([&](auto Kc) {
+    auto stageA = [&]() { static_for<Plan::count(gg, 0)>([&](auto Kc) {
       constexpr int id = Plan::nth(gg, 0, decltype(Kc)::value);
       constexpr typename Plan::Item it = Plan::item(id);
       constexpr int r = 2 * it.p;
@@ -430,22 +296,9 @@ __device__ __forceinline__ void chain_split(SplitX<NF>& XA, SplitX<NF>& XB, f32x
         uv[id][0] = fmaf(acc[it.j][r], inv.v[it.l], bv[id][0]);
         uv[id][1] = fmaf(acc[it.j][r + 1], inv.v[it.l], bv[id][1]);
       }
-#if defined(ECNF_SPLIT_IDENT_ACT)   // timing experiment: identity activation (split kept, SiLU arithmetic dropped)
-      ev[id][0] = 1.0f;
-      ev[id][1] = 1.0f;
-#elif defined(ECNF_SPLIT_NO_TRANS)   // timing experiment: the transcendentals replaced by plain VALU (same data flow)
-      ev[id][0] = uv[id][0] * 0.5f;
-      ev[id][1] = uv[id][1] * 0.5f;
-#else
       ev[id][0] = __builtin_amdgcn_exp2f(uv[id][0]);
       ev[id][1] = __builtin_amdgcn_exp2f(uv[id][1]);
-#endif
-      if constexpr (NT == 2) {   // a second, independent tile on the same weight fragments
-        dv[id][0] = accT[it.j][r];
-        dv[id][1] = accT[it.j][r + 1];
-        e2v[id][0] = __builtin_amdgcn_exp2f(dv[id][0]);
-        e2v[id][1] = __builtin_amdgcn_exp2f(dv[id][1]);
-      } else if constexpr (NT) {
+      if constexpr (NT) {
         if constexpr (kBI) {
           dv[id][0] = accT[it.j][r];
           dv[id][1] = accT[it.j][r + 1];
@@ -455,67 +308,32 @@ __device__ __forceinline__ void chain_split(SplitX<NF>& XA, SplitX<NF>& XB, f32x
         }
       }
     }); };
-    // stage B
+    // stage B: the add as packed fp32 where the compiler keeps the pair in an aligned register pair (bit-identical;
+    // LJ13 27.14 -> 27.02 ms, profiles/round2/e3)
     auto stageB = [&](auto Late) { static_for<Plan::count_l(gg, 1, decltype(Late)::value)>([&](auto Kc) {
       constexpr int id = Plan::nth_l(gg, 1, decltype(Late)::value, decltype(Kc)::value);
-#if defined(ECNF_SPLIT_IDENT_ACT)
-#elif defined(ECNF_SPLIT_NO_TRANS)
-      ev[id][0] = 0.25f * (1.0f + ev[id][0]);
-      ev[id][1] = 0.25f * (1.0f + ev[id][1]);
-#elif defined(ECNF_SPLIT_PK)
-      {
-        const f32x2 s = ev[id] + 1.0f;   // v_pk_add_f32: one issue for the pair
-        ev[id][0] = __builtin_amdgcn_rcpf(s[0]);
-        ev[id][1] = __builtin_amdgcn_rcpf(s[1]);
-      }
-#else
-      ev[id][0] = __builtin_amdgcn_rcpf(1.0f + ev[id][0]);
-      ev[id][1] = __builtin_amdgcn_rcpf(1.0f + ev[id][1]);
-#endif
-      if constexpr (NT == 2) {
-        e2v[id][0] = __builtin_amdgcn_rcpf(1.0f + e2v[id][0]);
-        e2v[id][1] = __builtin_amdgcn_rcpf(1.0f + e2v[id][1]);
-      }
+      const f32x2 s = ev[id] + 1.0f;
+      ev[id][0] = __builtin_amdgcn_rcpf(s[0]);
+      ev[id][1] = __builtin_amdgcn_rcpf(s[1]);
     }); };
     // stage C
     auto stageC = [&](auto Late) { static_for<Plan::count_l(gg, 2, decltype(Late)::value)>([&](auto Kc) {
       constexpr int id = Plan::nth_l(gg, 2, decltype(Late)::value, decltype(Kc)::value);
       constexpr typename Plan::Item it = Plan::item(id);
-#ifdef ECNF_SPLIT_IDENT_ACT
-      const float y0 = uv[id][0], y1 = uv[id][1];
-#elif defined(ECNF_SPLIT_PK)
-      const f32x2 yv = uv[id] * ev[id];   // v_pk_mul_f32
+      const f32x2 yv = uv[id] * ev[id];
       const float y0 = yv[0], y1 = yv[1];
-#else
-      const float y0 = uv[id][0] * ev[id][0];
-      const float y1 = uv[id][1] * ev[id][1];
-#endif
       if constexpr (it.l < NL - 1) {
         put_pair<NF, it.j, 2 * it.p>(pick<(it.l + 1) & 1>(XA, XB), y0, y1);
       } else {
         acc[it.j][2 * it.p] = y0;
         acc[it.j][2 * it.p + 1] = y1;
       }
-      if constexpr (NT == 2) {
-        const float z0 = dv[id][0] * e2v[id][0];
-        const float z1 = dv[id][1] * e2v[id][1];
-        if constexpr (it.l < NL - 1) {
-          put_pair<NF, it.j, 2 * it.p>(pick<(it.l + 1) & 1>(XAT, XBT), z0, z1);
-        } else {
-          accT[it.j][2 * it.p] = z0;
-          accT[it.j][2 * it.p + 1] = z1;
-        }
-      } else if constexpr (NT) {
+      if constexpr (NT) {
         constexpr float kNegLn2 = -0.69314718055994531f;
         // u (1 - r) = u - y' (y' = u r): 4 VALU per element instead of 5
-#ifdef ECNF_SPLIT_PK
         const f32x2 dd = (ev[id] * dv[id]) * __builtin_elementwise_fma(uv[id] - (f32x2){y0, y1}, (f32x2)kNegLn2,
                                                                       (f32x2)1.0f);
         const float d0 = dd[0], d1 = dd[1];
-#else
-        const float d0 = ev[id][0] * dv[id][0] * fmaf(uv[id][0] - y0, kNegLn2, 1.0f);
-        const float d1 = ev[id][1] * dv[id][1] * fmaf(uv[id][1] - y1, kNegLn2, 1.0f);
-#endif
         if constexpr (it.l < NL - 1) {
           put_pair<NF, it.j, 2 * it.p>(pick<(it.l + 1) & 1>(XAT, XBT), d0, d1);
         } else {
@@ -524,13 +342,11 @@ __device__ __forceinline__ void chain_split(SplitX<NF>& XA, SplitX<NF>& XB, f32x
         }
       }
     }); };
-#endif
-#if !defined(ECNF_SPLIT_SGB) && !defined(ECNF_SPLIT_CHEAP_ACT) && !defined(ECNF_SPLIT_NO_ACT)
     // Emission order pinned per MFMA gap: one stage per MFMA of the group (stage C, B, A after the 1st, 2nd, 3rd
     // MFMA term: each ~20 cycles of issue for one item, inside the 24 free issue cycles of a 32-cycle MFMA), every
     // gap closed by a sched_barrier.  Stage C consumes the rcp of the previous group, stage A reads an accumulator
-    // finished at least one group earlier, so no gap waits on its own MFMA.  (The sched_group_barrier form,
-    // -DECNF_SPLIT_SGB, left 2/3 of the gaps empty and bunched 40-100 issue cycles into the others.)
+    // finished at least one group earlier, so no gap waits on its own MFMA.  (A sched_group_barrier form left 2/3 of
+    // the gaps empty and bunched 40-100 issue cycles into the others.)
     if constexpr (mfma_group) {
       __builtin_amdgcn_sched_barrier(0);
       static_for<kTerms>([&](auto Tc) {
@@ -554,47 +370,6 @@ __device__ __forceinline__ void chain_split(SplitX<NF>& XA, SplitX<NF>& XB, f32x
       stageC(std::false_type{});
       stageC(std::true_type{});
     }
-#else
-    if constexpr (mfma_group) static_for<kTerms>([&](auto Tc) { mfma_t(Tc); });
-#if !defined(ECNF_SPLIT_CHEAP_ACT) && !defined(ECNF_SPLIT_NO_ACT)
-    stageA();
-    stageB(std::false_type{});
-    stageB(std::true_type{});
-    stageC(std::false_type{});
-    stageC(std::true_type{});
-#endif
-    if constexpr (mfma_group) {
-      // schedule: weight loads, bias reads, then MFMA / VALU alternating
-      constexpr int nvalu = (4 + 2 * NT) * nA + 4 * nB + (3 + 11 * NT) * nC;
-      constexpr int nmfma = kTerms * (1 + NT) + (WP == 3 ? 1 : 0);
-      constexpr int per = (nvalu + nmfma - 1) / nmfma;
-#ifndef ECNF_SPLIT_NO_SGB
-#if defined(ECNF_SPLIT_WLDS)
-      if constexpr (gg + PF < G) __builtin_amdgcn_sched_group_barrier(0x100, kPieces, 0);
-#elif !defined(ECNF_SPLIT_NO_WLOAD)
-      if constexpr (gg + PF < G) __builtin_amdgcn_sched_group_barrier(0x020, WP, 0);
-#endif
-      if constexpr (nbias > 0) __builtin_amdgcn_sched_group_barrier(0x100, nbias, 0);
-      if constexpr (load_cb) __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
-      static_for<nmfma>([&](auto) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        if constexpr (per > 0) __builtin_amdgcn_sched_group_barrier(0x002, per, 0);
-      });
-#endif
-      __builtin_amdgcn_sched_barrier(0);
-    }
-#endif
-#ifdef ECNF_SPLIT_RING
-    if constexpr (mfma_group && gg % kRingIV == kRingIV - 1) {
-      constexpr int iv = gg / kRingIV;
-      if constexpr ((iv + 1) * kRingIV < G) {
-        ring_store(iv + 1);
-        __syncthreads();
-        if constexpr ((iv + 2) * kRingIV < G) ring_fetch(iv + 2);
-        ring_read(gg + 1, wbuf[(gg + 1) % (PF + 1)]);
-      }
-    }
-#endif
   });
   __builtin_amdgcn_s_setprio(0);
 }
@@ -658,15 +433,13 @@ __device__ __forceinline__ void split_blocks(const f32x16 (&X)[NF], SplitX<NF>& 
 
 // weight groups in flight in dual_pass: 3 pieces x (PF + 1) slots beside the split input, the accumulators and the
 // other operand's fp32 activations (512-register waves)
-#ifndef ECNF_DUAL_PF
-#define ECNF_DUAL_PF 2
-#endif
+constexpr int kDualPF = 2;
 // one pass of one layer over the 3-piece exact weights (chain_split WP = 3): acc[jb] = sum over (fb, u) of
 // W[l][jb][fb][u] X'[fb][u] with the w2 x0 term in the PRIMAL pass (the tangent pass keeps three terms)
 template <int NF, bool PRIMAL>
 __device__ __forceinline__ void dual_pass(const SplitX<NF>& X, f32x16 (&acc)[NF], __amdgpu_buffer_rsrc_t rsrc,
                                           int voff, int layer_soff) {
-  constexpr int G = 2 * NF * NF, PF = ECNF_DUAL_PF, WP = 3;
+  constexpr int G = 2 * NF * NF, PF = kDualPF, WP = 3;
   u32x4 wbuf[PF + 1][WP];
   static_for<PF>([&](auto Gc) {
     constexpr int gg = decltype(Gc)::value;

@@ -14,6 +14,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <atomic>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -265,9 +266,10 @@ struct ecnf_handle {
   bool arena_used;
   hipStream_t arena_stream;
   // team (latency) mode of the primal kernels (egnn_eval.hpp team_exchange): exchange slots and the per-molecule
-  // arrival counters / timeout flags, allocated at create for up to team_cap molecules of team_gcap workgroups;
-  // shared by every ecnf_integrate on the handle (ordered across streams by team_ev under team_mu)
-  int team_mode;        // ecnf_set_team: 0 auto, 1 off, G >= 2 forced
+  // arrival counters / timeout flags for up to team_cap molecules of team_gcap workgroups, allocated at create only
+  // for shapes with a team kernel (team_shape) whose weights the split kernels represent; shared by every
+  // ecnf_integrate on the handle (ordered across streams by team_ev under team_mu)
+  std::atomic<int> team_mode;   // ecnf_set_team: 0 auto, 1 off, G >= 2 forced; read once per solve (team_size)
   int team_cap, team_gcap, team_slot;
   float* team_buf;
   unsigned* team_sync;  // [team_cap] counters, then [team_cap] timeout flags (one 16-B-padded block, zeroed per launch)
@@ -289,27 +291,8 @@ struct Packer {
   }
 };
 
-// bf16 round-to-nearest-even of a finite float, and back
-static inline uint16_t bf16_rne(float f) {
-  uint32_t u;
-  std::memcpy(&u, &f, 4);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (uint16_t)(u >> 16);
-}
-static inline float bf16_float(uint16_t b) {
-  const uint32_t u = (uint32_t)b << 16;
-  float f;
-  std::memcpy(&f, &u, 4);
-  return f;
-}
-
-// the power-of-two scale s of a split weight matrix (chain_split.hpp): max |w s| in [2^12, 2^13) for fp16 pieces,
-// 1 for bf16 pieces (fp32's exponent range)
+// the power-of-two scale s of a split weight matrix (chain_split.hpp): max |w s| in [2^12, 2^13) for fp16 pieces
 static float split_scale(const float* W, size_t n, size_t ld = 0, size_t cols = 0) {
-#ifdef ECNF_SPLIT_BF16
-  (void)W; (void)n; (void)ld; (void)cols;
-  return 1.0f;
-#else
   float mx = 0.f;
   for (size_t i = 0; i < n; ++i) {
     const float a = std::fabs(ld ? W[(i / cols) * ld + (i % cols)] : W[i]);
@@ -318,27 +301,17 @@ static float split_scale(const float* W, size_t n, size_t ld = 0, size_t cols = 
   if (!(mx > 0.f) || !std::isfinite(mx)) return 1.0f;
   const int e = std::max(-100, std::min(100, 12 - std::ilogb(mx)));
   return std::ldexp(1.0f, e);
-#endif
 }
 
 // w s = piece0 + ... by successive RNE; stores 16-bit element j of a lane's 8-element fragment, pieces
 // piece_stride u32 apart
 static inline void put_split(uint32_t* frag_p0, size_t piece_stride, int j, float w, float scale) {
   uint16_t piece[kPieces];
-#ifdef ECNF_SPLIT_BF16
-  (void)scale;
-  piece[0] = bf16_rne(w);
-  const float r1 = w - bf16_float(piece[0]);
-  piece[1] = bf16_rne(r1);
-  const float r2 = r1 - bf16_float(piece[1]);
-  piece[2] = bf16_rne(r2);
-#else
   const float ws = w * scale;   // exact (power of two, no overflow by construction)
   const _Float16 h0 = (_Float16)ws;
   const _Float16 h1 = (_Float16)(ws - (float)h0);
   std::memcpy(&piece[0], &h0, 2);
   std::memcpy(&piece[1], &h1, 2);
-#endif
   for (int p = 0; p < kPieces; ++p) {
     uint32_t& word = frag_p0[p * piece_stride + (j >> 1)];
     word = (j & 1) ? ((word & 0x0000ffffu) | ((uint32_t)piece[p] << 16)) : ((word & 0xffff0000u) | piece[p]);
@@ -467,21 +440,13 @@ void set_mpw(Net& n, const ecnf_cfg& c, int NT, int P, int mpw, int rp) {
     }
 }
 
-// static LDS of the integrate kernels beside the dynamic carve-up (ecnf_kernels.hpp solver_sizes, egnn_eval.hpp
-// half_bar_words), reserved when a configuration is sized against the CU's 160 KiB
+// static LDS of the integrate kernels beside the dynamic carve-up (ecnf_kernels.hpp solver_sizes), reserved when a
+// configuration is sized against the CU's 160 KiB
 constexpr size_t kStaticLdsBytes = 64;
 
 int choose_mpw(const ecnf_cfg& c, int NT, int P, int* mpw_out, size_t* lds_out, int* rp_out) {
   const int N = c.n_nodes, D = c.dim, H = c.hidden, T = c.time_embedding_dim, M = c.mlp_width;
   const int E = N * (N - 1), SR = edge_slots_per_receiver(N);
-  // experiment builds only (tools/build_timing.sh DEVFLAGS): -DECNF_FORCE_MPW / -DECNF_FORCE_MPW_TANGENT
-#ifndef ECNF_FORCE_MPW
-#define ECNF_FORCE_MPW 0
-#endif
-#ifndef ECNF_FORCE_MPW_TANGENT
-#define ECNF_FORCE_MPW_TANGENT 0
-#endif
-  const int forced = NT ? ECNF_FORCE_MPW_TANGENT : ECNF_FORCE_MPW;
   double best = -1;
   int best_m = 0;
   size_t best_lds = 0;
@@ -498,13 +463,12 @@ int choose_mpw(const ecnf_cfg& c, int NT, int P, int* mpw_out, size_t* lds_out, 
     const int EP = 32 * ((N * SR + 31) / 32);
     const int tiles = m * EP / 32;
     const double eff = (double)tiles / (kSimds * ((tiles + kSimds - 1) / kSimds)) * (double)(m * E) / (tiles * 32.0);
-    if (forced ? m == forced : eff > best + 1e-9) {
+    if (eff > best + 1e-9) {
       best = eff;
       best_m = m;
       best_lds = bytes;
       best_rp = RP;
     }
-    if (forced && m == forced) break;
   }
   if (!best_m) return fail(ECNF_E_UNSUPPORTED, "configuration does not fit the 160 KiB LDS of one CU");
   *mpw_out = best_m;
@@ -540,11 +504,8 @@ bool shape_supported(const ecnf_cfg& c, int NT, int P = -1) {
 // over the CUs as they retire, so the model charges (workgroups / CUs) continuous rounds, plus a per-workgroup
 // penalty per extra molecule for the expected max of m step counts (0: measured on ALDP B = 512 PID, penalty
 // 0 / 0.15 / 0.3 -> sample 3.23 / 3.73 / 3.70 ms, Hutchinson log_prob 57.9 / 58.0 / 58.1 ms,
-// profiles/round2/mpw_ab.log; -DECNF_ADAPTIVE_MPW_PENALTY=x in experiment builds).
-#ifndef ECNF_ADAPTIVE_MPW_PENALTY
-#define ECNF_ADAPTIVE_MPW_PENALTY 0.0
-#endif
-constexpr double adaptive_penalty() { return ECNF_ADAPTIVE_MPW_PENALTY; }
+// profiles/round2/mpw_ab.log).
+constexpr double adaptive_penalty() { return 0.0; }
 
 Net net_for_batch(const ecnf_handle* h, int ix, int B, size_t* lds, bool adaptive = false) {
   Net n = h->net[ix];
@@ -596,16 +557,17 @@ bool cols_fits(const ecnf_handle* h, int NT, int B) {
   return lds_bytes(c, 0, 0, 1, RP) + (size_t)cols_image_floats(c) * 4 + kStaticLdsBytes <= 160 * 1024;
 }
 
-int team_size(const ecnf_handle* h, int NT, int B, int* cols) {
+// mode: the handle's team_mode, read ONCE by the caller (a concurrent ecnf_set_team cannot split one solve's decision)
+int team_size(const ecnf_handle* h, int NT, int B, int* cols, int mode) {
   const ecnf_cfg& c = h->cfg;
   if (cols) *cols = 0;
-  if (NT != 0 || B < 1 || B > h->team_cap || h->team_mode == 1 ||
+  if (NT != 0 || B < 1 || B > h->team_cap || mode == 1 || !h->team_buf ||
       !team_shape(c.mlp_width, NT, c.mlp_depth, c.dim, h->prec))
     return 1;
   const int tpm = h->net[0].EP / 32;
   int G;
-  if (h->team_mode >= 2) {
-    G = std::min(std::min(h->team_mode, h->team_gcap), tpm);
+  if (mode >= 2) {
+    G = std::min(std::min(mode, h->team_gcap), tpm);
   } else {
     if (h->cfg.mlp_width < 256) return 1;
     if (cols_fits(h, NT, B)) {
@@ -618,14 +580,13 @@ int team_size(const ecnf_handle* h, int NT, int B, int* cols) {
   return G;
 }
 
-hipError_t dispatch_integrate(const ecnf_handle* h, int NT, const SolveP& sp_in, const float* y0, const int32_t* feat,
-                              const float* eps, float* y1, float* dlogp, int32_t* nfe, int32_t* status, int B,
-                              hipStream_t stream) {
+// G, cols: team_size's decision for this solve (G = 1: the batch path)
+hipError_t dispatch_integrate(const ecnf_handle* h, int NT, const SolveP& sp_in, int G, int cols, const float* y0,
+                              const int32_t* feat, const float* eps, float* y1, float* dlogp, int32_t* nfe,
+                              int32_t* status, int B, hipStream_t stream) {
   const int M = h->cfg.mlp_width, L = h->cfg.mlp_depth, D = h->cfg.dim, P = h->prec, ix = 2 * P + NT;
   size_t lds = 0;
   SolveP sp = sp_in;
-  int cols = 0;
-  const int G = team_size(h, NT, B, &cols);
   Net net;
   if (G > 1) {
     net = h->net[ix];
@@ -648,19 +609,6 @@ hipError_t dispatch_integrate(const ecnf_handle* h, int NT, const SolveP& sp_in,
   } else {
     sp.team = TeamP{};
     net = net_for_batch(h, ix, B, &lds, sp.adaptive != 0);
-    // halves mode (integrate_kernel HALF): a workgroup of m = 2 m' molecules runs as two independent halves of m'
-    // (own LDS, solver and barriers), so one half's node phases overlap the other's edge chains
-    const int m = net.MPW;
-    if (ECNF_HALVES && NT == 0 && split_primal(h->cfg, 0, P) && primal_waves(h->cfg) == 8 && m % 2 == 0) {
-      const int mh = m / 2, RP = 32 * ((mh * h->cfg.n_nodes + 31) / 32);
-      const size_t lh = lds_bytes(h->cfg, 0, P, mh, RP);
-      if (2 * lh + kStaticLdsBytes <= 160 * 1024) {
-        set_mpw(net, h->cfg, 0, P, mh, RP);
-        net.lds_floats = (int)(lh / 4);
-        lds = lh;
-        sp.halves = 1;
-      }
-    }
   }
 #define ECNF_CALL(m, l, d, nt, p) \
   launch_integrate<m / 32, nt, l, d, p>(net, lds, sp, y0, feat, eps, y1, dlogp, nfe, status, B, stream)
@@ -881,7 +829,7 @@ int ecnf_create(const ecnf_cfg* cfg, const float* params, size_t n_floats, int d
   bool split_ok = true;   // every edge-chain weight fits the unscaled fp16 split (|w| < 2^15)
   struct Off {
     size_t Wn, bn, Wp, bp, wd, We, Ws, be, wx, wg, Wh[kMaxPhiH], bh[kMaxPhiH], Wn_s, Wp_s, Wh_s[kMaxPhiH];
-    size_t bp_u, wd_u, be_u, wg_u, wx_u, Wh_sn0, W1_s, Ws3, bnp_u;
+    size_t bp_u, wd_u, be_u, wg_u, wx_u, Wh_sn0, W1_s, Ws3;
     float bx, bg, hinv_n0, w1inv;
     float cinv[2 * 4 - 1], ninv, pinv, hinv[kMaxPhiH];
   };
@@ -915,30 +863,8 @@ int ecnf_create(const ecnf_cfg* cfg, const float* params, size_t n_floats, int d
       for (auto& x : r) x *= f;
       return r;
     };
-    if (ECNF_FUSED_P) {
-      // fused node Dense + phi_e.0 halves (Geo::kFusedP): -log2(e) x W_n W_p over the [h | temb] rows and the bias
-      // -log2(e) x (b_n W_p + [0 | b1]), products in double, rounded once
-      std::vector<double> acc((size_t)(H + T) * 2 * M, 0.0), bacc(2 * M, 0.0);
-      for (int r = 0; r < H + T; ++r)
-        for (int q = 0; q < H; ++q) {
-          const double a = b.nk[(size_t)r * H + q];
-          for (int j = 0; j < 2 * M; ++j) acc[(size_t)r * 2 * M + j] += a * wp[(size_t)q * 2 * M + j];
-        }
-      for (int j = 0; j < 2 * M; ++j) {
-        double v = bp[j];
-        for (int q = 0; q < H; ++q) v += (double)b.nb[q] * wp[(size_t)q * 2 * M + j];
-        bacc[j] = v;
-      }
-      std::vector<float> wnp_u(acc.size()), bnp_u(2 * M);
-      for (size_t i = 0; i < acc.size(); ++i) wnp_u[i] = (float)(acc[i] * (double)kNegLog2e);
-      for (int j = 0; j < 2 * M; ++j) bnp_u[j] = (float)(bacc[j] * (double)kNegLog2e);
-      o.Wp_s = put_split_node(wnp_u.data(), H + T, 2 * M, &o.pinv);
-      o.bnp_u = pk.put(bnp_u.data(), bnp_u.size());
-    } else {
-      const std::vector<float> wp_u = scaled(wp.data(), wp.size(), kNegLog2e);
-      o.Wp_s = put_split_node(wp_u.data(), H, 2 * M, &o.pinv);
-      o.bnp_u = 0;
-    }
+    const std::vector<float> wp_u = scaled(wp.data(), wp.size(), kNegLog2e);
+    o.Wp_s = put_split_node(wp_u.data(), H, 2 * M, &o.pinv);
     // the M = 256 tangent kernels' per-edge phi_e.0: [h_s | h_r | |r|^2] rows 0 .. 2H of the kernel, x -log2(e)
     o.W1_s = put_split_node(scaled(b.ek[0], (size_t)(2 * H + 1) * M, kNegLog2e).data(), 2 * H + 1, M, &o.w1inv);
     o.bp_u = pk.put(scaled(bp.data(), bp.size(), kNegLog2e).data(), bp.size());
@@ -970,19 +896,13 @@ int ecnf_create(const ecnf_cfg* cfg, const float* params, size_t n_floats, int d
     for (int cl = 0; cl < 2 * 4 - 1; ++cl) o.cinv[cl] = 1.0f;
     for (int cl = 0; cl < nchain; ++cl) {
       const float* W = cl < L - 1 ? b.ek[cl + 1] : b.tk[cl - (L - 1)];
-#ifdef ECNF_CHAIN_BIAS_INIT
       // unscaled pieces: the chain adds the bias through the accumulator (chain_split.hpp); fp16 piece 0 must not
-      // overflow
       // overflow: such a network runs on the strict-fp32 kernels only (split_ok = false, see below)
       float mx = 0.f;
       for (size_t i = 0; i < (size_t)M * M; ++i) mx = std::max(mx, std::fabs(W[i]));
       if (!(mx < 32768.f)) split_ok = false;
-      const float sc = 1.0f;
-#else
-      const float sc = split_scale(W, (size_t)M * M);
-#endif
-      o.cinv[cl] = 1.0f / split_scale(W, (size_t)M * M);   // the 3-piece chain's scale (Ws3); sc = 1 is not read
-      pack_split_layer(W, M, sc, ws.data() + cl * split_layer);
+      o.cinv[cl] = 1.0f / split_scale(W, (size_t)M * M);   // the 3-piece chain's scale (Ws3); the 2-piece set is unscaled
+      pack_split_layer(W, M, 1.0f, ws.data() + cl * split_layer);
     }
     o.Ws = pk.put(reinterpret_cast<const float*>(ws.data()), ws.size());
     {   // the divergence kernels' exact 3-piece chain (scaled per layer)
@@ -1078,7 +998,6 @@ int ecnf_create(const ecnf_cfg* cfg, const float* params, size_t n_floats, int d
       w.Wh_sn0 = reinterpret_cast<const unsigned*>(dbuf + o.Wh_sn0);
       w.hinv_n0 = o.hinv_n0;
       w.W1_s = reinterpret_cast<const unsigned*>(dbuf + o.W1_s);
-      w.bnp_u = ECNF_FUSED_P ? dbuf + o.bnp_u : nullptr;
       w.w1inv = o.w1inv;
       w.Ws3 = reinterpret_cast<const unsigned*>(dbuf + o.Ws3);
     }
@@ -1099,7 +1018,9 @@ int ecnf_create(const ecnf_cfg* cfg, const float* params, size_t n_floats, int d
     return fail(ECNF_E_UNSUPPORTED, "configuration does not fit the LDS budget");
   }
   {
-    // team-mode buffers (team_size): up to kTeamCap molecules of up to team_gcap workgroups each
+    // team-mode buffers (team_size): up to kTeamCap molecules of up to team_gcap workgroups each, only where a team
+    // kernel exists (the split primal kernels of the BASELINE shapes) and the split kernels can run this parameter
+    // set (team_size returns 1 without them)
     const Net& n = h->net[0];
     const int tpm = n.EP / 32;
     h->team_cap = kTeamCap;
@@ -1107,7 +1028,8 @@ int ecnf_create(const ecnf_cfg* cfg, const float* params, size_t n_floats, int d
     h->team_gcap = c.mlp_width == 256 ? tpm : std::min(tpm, std::max(4, (tpm + primal_waves(c) - 1) / primal_waves(c)));
     h->team_slot = c.n_nodes * M + tpm * M + ((c.n_nodes * c.dim + 3) & ~3);
     const size_t nb = (size_t)h->team_cap * 2 * h->team_gcap * h->team_slot * sizeof(float);
-    if (hipMalloc(&h->team_buf, nb) != hipSuccess || hipMalloc(&h->team_sync, kTeamSyncBytes) != hipSuccess) {
+    const bool want = h->split_ok && team_shape(c.mlp_width, 0, c.mlp_depth, c.dim, 0);
+    if (want && (hipMalloc(&h->team_buf, nb) != hipSuccess || hipMalloc(&h->team_sync, kTeamSyncBytes) != hipSuccess)) {
       if (h->team_buf) hipFree(h->team_buf);
       hipFree(dbuf);
       delete h;
@@ -1143,6 +1065,11 @@ int ecnf_update_params(ecnf_handle* h, const float* params, int32_t on_device) {
   }
   h->split_ok = t->split_ok;
   if (!h->split_ok) h->prec = ECNF_PREC_FP32;
+  if (!h->team_buf && t->team_buf) {   // the new weights admit the split team kernels the old ones did not
+    std::lock_guard<std::mutex> tl(h->team_mu);
+    std::swap(h->team_buf, t->team_buf);
+    std::swap(h->team_sync, t->team_sync);
+  }
   return ecnf_destroy(t);
 }
 
@@ -1186,11 +1113,7 @@ int ecnf_chain_arithmetic(ecnf_handle* h, int32_t with_tangent, int32_t* mode) {
   const bool split = split_primal(h->cfg, with_tangent ? 1 : 0, h->prec) ||
                      (kSplitTanChain && h->prec == ECNF_PREC_SPLIT_F16 && with_tangent && h->cfg.mlp_width <= 128) ||
                      (kSplitTanChain && h->prec == ECNF_PREC_SPLIT_F16 && wide_tangent(h->cfg, with_tangent ? 1 : 0, h->prec));
-#ifdef ECNF_SPLIT_BF16
-  *mode = split ? ECNF_CHAIN_SPLIT_BF16 : ECNF_CHAIN_FP32_MFMA;
-#else
   *mode = split ? ECNF_CHAIN_SPLIT_F16 : ECNF_CHAIN_FP32_MFMA;
-#endif
   return ECNF_OK;
 }
 
@@ -1257,7 +1180,7 @@ int ecnf_set_team(ecnf_handle* h, int32_t mode) {
 
 int ecnf_team_workgroups(ecnf_handle* h, int32_t with_tangent, int32_t batch, int32_t* G) {
   if (!h || !G) return fail(ECNF_E_INVALID, "NULL argument");
-  *G = team_size(h, with_tangent ? 1 : 0, batch, nullptr);
+  *G = team_size(h, with_tangent ? 1 : 0, batch, nullptr, h->team_mode.load());
   return ECNF_OK;
 }
 
@@ -1325,7 +1248,9 @@ int integrate_impl(ecnf_handle* h, const ecnf_solve_opts* o, const float* y0, co
   sp.pcache = nullptr;
   sp.pcache_slots = 0;
   sp.team = TeamP{};   // dispatch_integrate sets it (team_size)
-  sp.halves = 0;       // ... and this (halves mode)
+  // team mode decided once for this solve: one read of the handle's mode (ecnf_set_team may run concurrently)
+  int cols = 0;
+  const int G = team_size(h, NT, batch, &cols, h->team_mode.load());
   const size_t need = sp.sparse1 ? pcache_floats(h, batch) : 0;
   // the arena pointer and size are read under arena_mu, and the lock is held through the dispatch that uses them:
   // an ecnf_reserve_workspace on another thread cannot free the arena between the read and the launch
@@ -1347,21 +1272,21 @@ int integrate_impl(ecnf_handle* h, const ecnf_solve_opts* o, const float* y0, co
     // (arena_mu, held since the arena was read)
     if (!h->arena_ev) HIP_TRY(hipEventCreateWithFlags(&h->arena_ev, hipEventDisableTiming));
     if (h->arena_used && h->arena_stream != stream) HIP_TRY(hipStreamWaitEvent(stream, h->arena_ev, 0));
-    HIP_TRY(dispatch_integrate(h, NT, sp, y0, feat, eps, y1, dlogp, nfe, status, batch, stream));
+    HIP_TRY(dispatch_integrate(h, NT, sp, G, cols, y0, feat, eps, y1, dlogp, nfe, status, batch, stream));
     HIP_TRY(hipEventRecord(h->arena_ev, stream));
     h->arena_used = true;
     h->arena_stream = stream;
-  } else if (team_size(h, NT, batch, nullptr) > 1) {
+  } else if (G > 1) {
     // team mode: the exchange slots and counters are shared by every solve on the handle (ordered as the arena)
     std::lock_guard<std::mutex> tl(h->team_mu);
     if (!h->team_ev) HIP_TRY(hipEventCreateWithFlags(&h->team_ev, hipEventDisableTiming));
     if (h->team_used && h->team_stream != stream) HIP_TRY(hipStreamWaitEvent(stream, h->team_ev, 0));
-    HIP_TRY(dispatch_integrate(h, NT, sp, y0, feat, eps, y1, dlogp, nfe, status, batch, stream));
+    HIP_TRY(dispatch_integrate(h, NT, sp, G, cols, y0, feat, eps, y1, dlogp, nfe, status, batch, stream));
     HIP_TRY(hipEventRecord(h->team_ev, stream));
     h->team_used = true;
     h->team_stream = stream;
   } else {
-    HIP_TRY(dispatch_integrate(h, NT, sp, y0, feat, eps, y1, dlogp, nfe, status, batch, stream));
+    HIP_TRY(dispatch_integrate(h, NT, sp, G, cols, y0, feat, eps, y1, dlogp, nfe, status, batch, stream));
   }
   g_err.clear();
   return ECNF_OK;

@@ -52,9 +52,6 @@ struct SolveP {
   // team (latency) mode of the primal kernels (egnn_eval.hpp team_exchange): team.G > 1 workgroups per molecule,
   // MPW = 1, grid = batch x G (a cooperative launch: every member co-resident)
   TeamP team;
-  // halves mode (integrate_kernel HALF): 1 = launch 512-thread workgroups of two independent 256-thread halves with
-  // net.MPW molecules and net.lds_floats floats of LDS each (the host sets it for halves_shape kernels)
-  int halves;
 };
 
 // solver state in LDS, after the eval region
@@ -95,7 +92,7 @@ __device__ __forceinline__ float uniform_f(float x) {
 // start and read at every use site in the loop (LDS loads after barriers), so they occupy no SGPRs across the
 // evaluations (kept in SGPRs, they were spilled through VGPRs to scratch in the 256-register kernels)
 __device__ __forceinline__ int* solver_sizes() {
-  __shared__ int sz[4];   // [MPW, ND, solver-state offset in floats from the half's LDS base, -]
+  __shared__ int sz[4];   // [MPW, ND, solver-state offset in floats from the dynamic LDS base, -]
   return sz;
 }
 __device__ __forceinline__ int solver_size(int k) { return __builtin_amdgcn_readfirstlane(solver_sizes()[k]); }
@@ -122,13 +119,13 @@ __device__ inline bool check_features(const Net& net, int* f) {
 
 // one evaluation of the joint field g(tau, y) = dir * f(dir * tau, y) at (st.ts, st.ys) for every molecule
 // of the workgroup; writes kx_out [MPW][ND] and kl_out [MPW].  Exactly one egnn_eval call site (it is inlined).
-template <int NF, int NT, int L, int D, int P, bool TEAM, bool HALF, bool COLS>
+template <int NF, int NT, int L, int D, int P, bool TEAM, bool COLS>
 __device__ __forceinline__ void joint_field(const Net& net, const Lds& s, const SolverLds& st, const SolveP& sp,
                                             float* kx_out, float* kl_out, const TeamCtx* tm, int* tepoch) {
-  constexpr int kThreads = HALF ? 256 : kernel_threads<NF, NT, P, COLS>();
+  constexpr int kThreads = kernel_threads<NF, NT, P, COLS>();
   // per-thread indices are re-derived (opaque_tid) on each side of the evaluation: kept live across it, they spill
   const int MPW = solver_size(0), ND = solver_size(1);
-  int tid = vtid<HALF>();
+  int tid = opaque_tid();
   // NT == 0: one primal eval; Hutchinson: one JVP along eps; exact: the trace of J from ND - D JVPs along e_k,
   // k >= D.  The field only sees relative positions and subtracts the input mean (egnn.py:176-188), so
   // v(x + s 1) = v(x) - s exactly, i.e. J T_c = -T_c for the translations T_c = sum_a e_(a,c).  In the basis
@@ -141,14 +138,14 @@ __device__ __forceinline__ void joint_field(const Net& net, const Lds& s, const 
   if (tid < MPW) st.divv[tid] = exact ? -(float)D : 0.f;
   for (int k0 = 0; k0 < nrep; ++k0) {
     const int k = exact ? k0 + D : k0;
-    tid = vtid<HALF>();
+    tid = opaque_tid();
     if constexpr (NT) {
       if (sp.div == ECNF_DIV_HUTCHINSON) {
         for (int i = tid; i < MPW * ND; i += kThreads) st.tin[i] = st.eps[i];
       } else {
         for (int i = tid, NDo = opaque_u(ND); i < MPW * NDo; i += kThreads) st.tin[i] = ((i % NDo) == k) ? 1.0f : 0.0f;
       }
-      wg_sync<HALF>();
+      __syncthreads();
     }
     // exact: the unit tangent e_k sits on atom k / D, so block 1 (whose node features carry no tangent) has nonzero
     // edge tangents only on the 2(N - 1) edges at that atom
@@ -157,9 +154,9 @@ __device__ __forceinline__ void joint_field(const Net& net, const Lds& s, const 
                     ? sp.pcache + (size_t)blockIdx.x * MPW * (net.N * (NF * 32) + 2 * net.N * D)
                     : nullptr;
     ECNF_DCHECK(!pc || (int)(blockIdx.x + 1) * MPW <= sp.pcache_slots, 6);
-    egnn_eval<NF, NT, L, D, P, TEAM, HALF, COLS>(net, s, st.ys, st.ts, st.tin, st.vout, st.tout, st.active, sparse ? k / D : -1,
+    egnn_eval<NF, NT, L, D, P, TEAM, COLS>(net, s, st.ys, st.ts, st.tin, st.vout, st.tout, st.active, sparse ? k / D : -1,
                                      pc, k0 == 0 ? 1 : 2, tm, tepoch);
-    tid = vtid<HALF>();
+    tid = opaque_tid();
     if constexpr (NT) {
       if (tid < MPW) {
         if (sp.div == ECNF_DIV_HUTCHINSON) {
@@ -172,13 +169,13 @@ __device__ __forceinline__ void joint_field(const Net& net, const Lds& s, const 
       }
     }
   }
-  tid = vtid<HALF>();
+  tid = opaque_tid();
   for (int i = tid; i < MPW * ND; i += kThreads) kx_out[i] = sp.dirf * st.vout[i];
   if (tid < MPW) {
     kl_out[tid] = sp.dirf * st.divv[tid];
     if (st.active[tid]) st.nfe[tid] += 1;
   }
-  wg_sync<HALF>();
+  __syncthreads();
 }
 
 // diffrax rms_norm over the leaves of one molecule's state: (x, logp) when the divergence is tracked
@@ -191,23 +188,15 @@ enum Phase { kEuler = 0, kInit0 = 1, kInit1 = 2, kFsal = 3, kStage = 4 };
 
 // The whole solve as a phase machine around ONE field evaluation per loop trip.  TEAM: the team (latency) mode
 // instantiation (egnn_eval.hpp team_exchange; launched only with sp.team.G > 1, compiled for team_shape)
-template <int NF, int NT, int L, int D, int P, bool TEAM = false, bool HALF = false, bool COLS = false>
-__global__ __launch_bounds__((HALF ? 512 : kernel_threads<NF, NT, P, COLS>())) __attribute__((amdgpu_waves_per_eu(Geo<NF, NT, P>::WPE))) void integrate_kernel(Net net, SolveP sp, const float* __restrict__ y0,
+template <int NF, int NT, int L, int D, int P, bool TEAM = false, bool COLS = false>
+__global__ __launch_bounds__((kernel_threads<NF, NT, P, COLS>())) __attribute__((amdgpu_waves_per_eu(Geo<NF, NT, P>::WPE))) void integrate_kernel(Net net, SolveP sp, const float* __restrict__ y0,
                                                                   const int32_t* __restrict__ feat,
                                                                   const float* __restrict__ eps, float* y1,
                                                                   float* dlogp, int32_t* nfe_out,
                                                                   int32_t* status_out, int B) {
-  // HALF (halves mode, egnn_eval.hpp wg_sync): two independent 256-thread halves, half h = threadIdx.x / 256 with
-  // its own net.lds_floats of LDS and molecules [(2 blockIdx + h) MPW, +MPW)
-  constexpr int kThreads = HALF ? 256 : kernel_threads<NF, NT, P, COLS>();
-  extern __shared__ float smem_all[];
-  const int half = HALF ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 8)) : 0;
-  if constexpr (HALF) {
-    if (threadIdx.x < 4) half_bar_words()[threadIdx.x] = 0;
-    __syncthreads();   // the only workgroup barrier of a halves kernel: both halves start together
-  }
-  float* smem = smem_all + (HALF ? half * net.lds_floats : 0);
-  const int tid = HALF ? (int)(threadIdx.x & 255) : (int)threadIdx.x, MPW = net.MPW, ND = net.ND, N = net.N;
+  constexpr int kThreads = kernel_threads<NF, NT, P, COLS>();
+  extern __shared__ float smem[];
+  const int tid = (int)threadIdx.x, MPW = net.MPW, ND = net.ND, N = net.N;
   const Lds s = carve_lds<NT, Geo<NF, NT, P>::kSplitN, Geo<NF, NT, P>::kNoP>(net, smem);
   const SolverLds st = carve_solver(s.tail, MPW, ND);
   // team mode: workgroup blockIdx = T G + r is member r of molecule T's team (MPW = 1); only member 0 writes outputs
@@ -219,16 +208,14 @@ __global__ __launch_bounds__((HALF ? 512 : kernel_threads<NF, NT, P, COLS>())) _
   const TeamCtx* tm = team ? &team_ctx : nullptr;
   int tepoch = 0;
   const bool writer_wg = team_ctx.r == 0;
-  const int mol0 = team ? team_ctx.T : HALF ? (2 * (int)blockIdx.x + half) * MPW : (int)blockIdx.x * MPW;
+  const int mol0 = team ? team_ctx.T : (int)blockIdx.x * MPW;
   const int nmol = min(MPW, B - mol0);
-  if constexpr (HALF)
-    if (nmol <= 0) return;   // the second half of the last workgroup has no molecules (it never syncs again)
   ECNF_DCHECK((int)(s.tail - smem) + solver_lds_floats(MPW, ND) <= net.lds_floats, 0);
   ECNF_DCHECK(nmol >= 1 && nmol <= MPW, 5);
 
   // zero the eval scratch (aggregates must start at +0; padding rows stay finite)
   for (int i = tid; i < (int)(s.tail - smem); i += kThreads) smem[i] = 0.f;
-  wg_sync<HALF>();
+  __syncthreads();
   for (int i = tid; i < MPW * ND; i += kThreads) {
     const int m = i / ND;
     st.y[i] = m < nmol ? y0[(size_t)mol0 * ND + i] : 0.f;
@@ -257,11 +244,11 @@ __global__ __launch_bounds__((HALF ? 512 : kernel_threads<NF, NT, P, COLS>())) _
     st.ctl[3] = sp.solver == ECNF_SOLVER_EULER ? kEuler : (sp.adaptive ? kInit0 : kFsal);
     st.ctl[4] = 1;
   }
-  wg_sync<HALF>();
+  __syncthreads();
   // device-side input check (no host sync on the call path): a molecule with an embedding id outside
   // [0, n_features) reports ECNF_E_INVALID (nn.Embed would index out of range) and is solved with id 0
   if (tid < nmol && !check_features(net, s.feat + tid * N)) st.status[tid] = ECNF_E_INVALID;
-  wg_sync<HALF>();
+  __syncthreads();
 
 
 #ifdef ECNF_STAMPS
@@ -272,7 +259,7 @@ __global__ __launch_bounds__((HALF ? 512 : kernel_threads<NF, NT, P, COLS>())) _
   }
 #endif
   while (true) {
-    const int tid = vtid<HALF>();   // shadows the kernel-level tid: nothing per-thread stays live across an eval
+    const int tid = opaque_tid();   // shadows the kernel-level tid: nothing per-thread stays live across an eval
     const int MPW = solver_size(0), ND = solver_size(1);   // (likewise the sizes, the solver-state pointers)
     const SolverLds st = carve_solver(smem + solver_size(2), MPW, ND);
     const int a = align4(MPW * ND), b = align4(MPW);
@@ -309,7 +296,7 @@ __global__ __launch_bounds__((HALF ? 512 : kernel_threads<NF, NT, P, COLS>())) _
           *st.any = any;
         }
         if (tid < MPW) st.h[tid] = st.tnext[tid] - st.tau[tid];
-        wg_sync<HALF>();
+        __syncthreads();
         if (*st.any == 0) break;
       }
       for (int i = tid; i < MPW * ND; i += kThreads) {
@@ -320,15 +307,15 @@ __global__ __launch_bounds__((HALF ? 512 : kernel_threads<NF, NT, P, COLS>())) _
       if (tid < MPW) st.ts[tid] = sp.dirf * (st.tau[tid] + kC[stage] * st.h[tid]);
       kx_out = st.kx + stage * a; kl_out = st.kl + stage * b;
     }
-    wg_sync<HALF>();
+    __syncthreads();
 
-    joint_field<NF, NT, L, D, P, TEAM, HALF, COLS>(net, s, st, sp, kx_out, kl_out, tm, &tepoch);
+    joint_field<NF, NT, L, D, P, TEAM, COLS>(net, s, st, sp, kx_out, kl_out, tm, &tepoch);
 
     // ------------------------------------------------ consume it
     {
     // per-thread indices, solver pointers and the control state re-derived after the evaluation (nothing of the
     // trip's first half stays live across it)
-    const int tid = vtid<HALF>();
+    const int tid = opaque_tid();
     const int MPW = solver_size(0), ND = solver_size(1);
     const SolverLds st = carve_solver(smem + solver_size(2), MPW, ND);
     const int a = align4(MPW * ND), b = align4(MPW);
@@ -426,7 +413,7 @@ __global__ __launch_bounds__((HALF ? 512 : kernel_threads<NF, NT, P, COLS>())) _
         st.dt[m] = new_dt;
         st.h0[m] = (float)new_atmin;
       }
-      wg_sync<HALF>();
+      __syncthreads();
       for (int i = tid; i < MPW * ND; i += kThreads) {
         const int m = i / ND;
         if (st.keep[m]) {
@@ -463,10 +450,10 @@ __global__ __launch_bounds__((HALF ? 512 : kernel_threads<NF, NT, P, COLS>())) _
       st.ctl[3] = phase;
       st.ctl[4] = stage;
     }
-    wg_sync<HALF>();
+    __syncthreads();
     }   // consume
   }
-  wg_sync<HALF>();
+  __syncthreads();
 #ifdef ECNF_STAMPS
   if (threadIdx.x == 0) {
     STAMP(s, kStSolver);
@@ -480,7 +467,7 @@ __global__ __launch_bounds__((HALF ? 512 : kernel_threads<NF, NT, P, COLS>())) _
   // overflowing field) is reported per molecule instead of passing as ECNF_OK.  (tid and the solver-state pointers
   // re-derived here: kept from the kernel's start, they would stay live across the whole solve and spill.)
   {
-  const int tid = vtid<HALF>();
+  const int tid = opaque_tid();
   const SolverLds st = carve_solver(smem + solver_size(2), MPW, ND);
   if (tid < nmol && st.status[tid] == ECNF_OK) {
     bool fin = isfinite(st.lp[tid]);
@@ -492,7 +479,7 @@ __global__ __launch_bounds__((HALF ? 512 : kernel_threads<NF, NT, P, COLS>())) _
     if (tid == 0 && __hip_atomic_load((ECNF_GLOBAL int*)(sp.team.timeout + team_ctx.T), __ATOMIC_RELAXED,
                                       __HIP_MEMORY_SCOPE_AGENT))
       st.status[0] = ECNF_E_HIP;
-    wg_sync<HALF>();
+    __syncthreads();
     if (!writer_wg) return;
   }
   for (int i = tid; i < nmol * ND; i += kThreads) y1[(size_t)mol0 * ND + i] = st.y[i];
@@ -551,18 +538,6 @@ __global__ __launch_bounds__((Geo<NF, NT, P>::NTHR)) __attribute__((amdgpu_waves
   }
 }
 
-// halves-mode kernels (integrate_kernel HALF): the 8-wave split primal kernels (M <= 128).  Measured, not adopted
-// (DESIGN 3.10 / 5.3): LJ13 B = 1024 Euler-100 28.17 ms against 26.78 ms for the 8-wave kernel (interleaved A/B), and
-// the ALDP PID sample built with it returned NaNs after barrier timeouts (not investigated further); -DECNF_HALVES=1
-// builds them
-#ifndef ECNF_HALVES
-#define ECNF_HALVES 0
-#endif
-template <int NF, int NT, int P>
-constexpr bool halves_shape() {
-  return ECNF_HALVES && NT == 0 && Geo<NF, NT, P>::kSplit && NF <= 4 && Geo<NF, NT, P>::NW == 8;
-}
-
 // shapes with a team-mode kernel (ecnf_hip.hip team_size): the split primal kernels of the BASELINE networks
 // (QM9 M = 256, LJ13 M = 128, ALDP M = 64)
 constexpr bool team_shape(int M, int NT, int L, int D, int P) {
@@ -584,7 +559,7 @@ hipError_t launch_integrate(const Net& net, size_t lds, const SolveP& sp, const 
     // launch checks the grid against the occupancy query (hipErrorCooperativeLaunchTooLarge instead of a hang)
     auto kt = integrate_kernel<NF, NT, L, D, P, true>;
     if constexpr (cols_shape(NF * 32, NT, L, D, P)) {
-      if (sp.team.cols) kt = integrate_kernel<NF, NT, L, D, P, true, false, true>;
+      if (sp.team.cols) kt = integrate_kernel<NF, NT, L, D, P, true, true>;
     }
     if (sp.team.cols && !cols_shape(NF * 32, NT, L, D, P)) return hipErrorInvalidValue;
     hipError_t e = hipFuncSetAttribute((const void*)kt, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -601,17 +576,6 @@ hipError_t launch_integrate(const Net& net, size_t lds, const SolveP& sp, const 
     }
   }
   if (sp.team.G > 1) return hipErrorInvalidValue;   // no team kernel for this shape (team_size never asks for one)
-  if constexpr (halves_shape<NF, NT, P>()) {
-    if (sp.halves) {
-      auto kh = integrate_kernel<NF, NT, L, D, P, false, true>;
-      hipError_t e = hipFuncSetAttribute((const void*)kh, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(2 * lds));
-      if (e != hipSuccess) return e;
-      const int grid = (B + 2 * net.MPW - 1) / (2 * net.MPW);
-      hipLaunchKernelGGL(kh, dim3(grid), dim3(512), 2 * lds, stream, net, sp, y0, feat, eps, y1, dlogp, nfe, status, B);
-      return hipGetLastError();
-    }
-  }
-  if (sp.halves) return hipErrorInvalidValue;
   auto k = integrate_kernel<NF, NT, L, D, P>;
   hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;

@@ -33,41 +33,22 @@
 namespace ecnf {
 
 constexpr int kSimds = 4;   // SIMDs per CU
-// Edge-chain arithmetic: the primal kernels with M <= 128 run the chain on the bf16 matrix cores with
-// fp32-accurate operand splitting (chain_split.hpp); -DECNF_FP32_CHAIN builds the fp32-MFMA chain instead.
-#ifdef ECNF_FP32_CHAIN
-constexpr bool kSplitChain = false;
-#else
+// Edge-chain arithmetic: the primal and tangent kernels of the default precision run their chains on the 16-bit
+// matrix cores with fp32-accurate operand splitting (chain_split.hpp); the strict-fp32 kernels (P = 1) on
+// v_mfma_f32_32x32x2_f32.
 constexpr bool kSplitChain = true;
-#endif
 // Waves per workgroup.  Split primal kernels: 8 waves = 2 per SIMD (<= 256 registers each): one wave's VALU and
 // LDS phases (activations, gate / aggregation scans, layer-1 gathers) overlap the other wave's MFMA chain
 // (measured 31.5 -> 28.6 ms at LJ13 over 4 waves with 512 registers).  fp32-MFMA chain, primal, M <= 128: 8 waves.
 // Tangent kernels and the split M = 256 chain (QM9: 3 x 128 registers of split input / output / accumulators per
 // tile) need up to 512 registers: 4 waves, 1 per SIMD (QM9 B = 2048 Euler-100: fp32 MFMA 7203 ms -> split 2271 ms).
-#ifdef ECNF_FP32_TANGENT_CHAIN
-constexpr bool kSplitTanChain = false;
-#else
 constexpr bool kSplitTanChain = kSplitChain;
-#endif
-#ifndef ECNF_SPLIT_MAX_NF
-#define ECNF_SPLIT_MAX_NF 8
-#endif
-constexpr int kSplitMaxNF = ECNF_SPLIT_MAX_NF;   // split chain up to M = 32 kSplitMaxNF
-// k-steps of node-GEMM A fragments in flight (node_task_split; Geo::kNodePFA)
-#ifndef ECNF_NODE_PFA_WIDE   // (A/B pending: 6 for the M = 256 split primal kernels, tools/libt_q6 vs libt_q2)
-#define ECNF_NODE_PFA_WIDE 2
-#endif
-#ifndef ECNF_NODE_PFA
-#define ECNF_NODE_PFA 2
-#endif
-// Tangent kernels' node GEMMs (node Dense, the phi_e.0 halves, phi_h) on the split path; -DECNF_FP32_TANGENT_NODE
-// keeps them on v_mfma_f32_32x32x2_f32.
-#ifdef ECNF_FP32_TANGENT_NODE
-constexpr bool kSplitTanNode = false;
-#else
+constexpr int kSplitMaxNF = 8;   // split chain up to M = 32 kSplitMaxNF
+// k-steps of node-GEMM A fragments in flight (node_task_split; Geo::kNodePFA).  Measured: depth 2 / 4 / 6 of the M = 256
+// kernels 311 / 314 / 322 us per QM9 cols evaluation (profiles/round4/r4w); LJ13 2 / 4 / 6 within noise (r4k)
+constexpr int kNodePFADefault = 2;
+// Tangent kernels' node GEMMs (node Dense, the phi_e.0 halves, phi_h) on the split path (M <= 128)
 constexpr bool kSplitTanNode = true;
-#endif
 // P: GEMM arithmetic of the kernel.  P = 0 (ECNF_PREC_SPLIT_F16, the default) as described above; P = 1
 // (ECNF_PREC_FP32, ecnf_set_precision) every GEMM on v_mfma_f32_32x32x2_f32 with fp32 operands: the strict-fp32
 // comparator and the fallback for molecules whose activations leave the fp16 range (ECNF_E_NONFINITE).
@@ -89,51 +70,30 @@ struct Geo {
   static constexpr bool kWideT32 = P == 1 && NT == 1 && NF == 8;
   static constexpr bool kNoP = kWideT || kWideT32;   // no per-node phi_e.0 halves (P rows) in LDS
   static constexpr bool kSplitN = kSplit || (kSplitTanNode && kSplitT) || kWideT;
-#ifndef ECNF_FUSED_P
-#define ECNF_FUSED_P 0
-#endif
-  // experiment (-DECNF_FUSED_P=1, measured, not adopted): the split kernels with per-node phi_e.0 halves compute them
-  // from hin with the host-fused W_n W_p in the same node phase as the node Dense (one barrier and one GEMM latency
-  // less per block, but K = H + T instead of H for the P GEMM): LJ13 26.02 vs 25.92 ms, LJ13 Hutchinson 63.84 vs
-  // 63.89, ALDP PID sample 3.25 vs 3.21, ALDP Hutchinson 29.84 vs 30.51 ms (profiles/round3/ab/tvf_*.log)
-  static constexpr bool kFusedP = ECNF_FUSED_P && kSplitN && !kNoP;
   // M <= 128 split tangent kernels: P (primal and tangent rows) in the log2 domain (the primal kernels' -log2(e)
   // fragments), phi_e.0's SiLU and its tangent evaluated there and split straight into the chain's input buffers
   static constexpr bool kL2T = kSplitT && kSplitN;
-#ifndef ECNF_SPLIT_NW
-#define ECNF_SPLIT_NW 8
-#endif
-#ifndef ECNF_COLS_NW
+  // M <= 128 primal kernels: 8 waves (2 per SIMD, 256 registers: one wave's VALU / LDS phases beside the other's chain,
+  // 31.5 -> 28.6 ms at LJ13 over 4 waves with 512 registers; two 4-wave workgroups per CU measured 29.4 ms).
+  // M = 64 tangent kernels (ALDP): 8 waves too, so one wave's VALU phases (layer-1 assembly, gate / aggregation
+  // scans, shifts: twice the VALU per MFMA of M = 128) overlap the other's chain (ALDP B = 512 PID Hutchinson log_prob
+  // 61.8 -> 50.2 ms, outputs bitwise equal).  The M = 128 tangent kernels (1.2 KB per lane of spills at 256
+  // registers) and the M = 256 kernels (968 B per lane at 2 waves per SIMD; QM9 2162 -> 3423 ms) run 4 waves.
+  static constexpr int NW = (NT == 0 && NF <= 4) ? 8 : (NT == 1 && P == 0 && NF <= 2 ? 8 : 4);
+  static constexpr int NTHR = 64 * NW;
+  // minimum waves per SIMD the register allocation must allow (the 8-wave tangent kernels: 256 registers)
+  static constexpr int WPE = (NT == 1 && NW == 8) ? 2 : 1;
+  // k-steps of node-GEMM A fragments in flight (node_task_split)
+  static constexpr int kNodePFA = kNodePFADefault;
+};
 // waves of the column-split team kernel (M = 256 split primal): 8, one output block of each chain layer per wave, two
 // waves per SIMD to hide the fragment stream (QM9 B = 1 Euler-20: 456 -> 311 us per evaluation, bitwise equal;
 // profiles/round4/r4q).  The batch-path and tile-dealt M = 256 kernels stay at 4 waves: at 8 they spill 828 B per
 // lane (2283 -> 2587 us per evaluation).
-#define ECNF_COLS_NW 8
-#endif
-#ifndef ECNF_TAN_NW_NF2
-#define ECNF_TAN_NW_NF2 8
-#endif
-  // M = 64 tangent kernels (ALDP): 8 waves, 2 per SIMD at <= 256 registers, so one wave's VALU phases (layer-1
-  // assembly, gate / aggregation scans, shifts: twice the VALU per MFMA of M = 128) overlap the other's chain
-  // (ALDP B = 512 PID Hutchinson log_prob 61.8 -> 50.2 ms, outputs bitwise equal; 72 B/lane of spills outside the
-  // chain)
-  // (M = 128 at 8 waves: even with sequential primal / tangent chain passes, chain_dual_seq, the kernel spilled
-  // 1.2 KB per lane at 256 registers; it stays at 4 waves)
-  static constexpr int NW = (NT == 0 && NF <= 4) ? (kSplit ? ECNF_SPLIT_NW : 8)
-                            : (NT == 1 && P == 0 && NF <= 2 ? ECNF_TAN_NW_NF2 : 4);
-  static constexpr int NTHR = 64 * NW;
-  // minimum waves per SIMD the register allocation must allow: 2 only for 2 x 4-wave workgroups per CU of the M <= 128
-  // split primal kernels at -DECNF_SPLIT_NW=4.  (The M = 256 split primal kernels also run 4 waves, but need their
-  // 512 registers: at 2 waves per SIMD they spilled 968 B per lane and QM9 B = 2048 Euler-100 ran 2162 -> 3423 ms.)
-  static constexpr int WPE = ((kSplit && NF <= 4 && NW == 4) || (NT == 1 && NW == 8)) ? 2 : 1;
-  // k-steps of node-GEMM A fragments in flight (node_task_split): the M = 256 split primal kernels (4 waves, 512
-  // registers; their node GEMMs stream 64 KiB of fragments per wave from L2 per GEMM: QM9's latency path is made of
-  // them) run a deeper ring than the 256-register kernels
-  static constexpr int kNodePFA = (kSplit && NF == 8) ? ECNF_NODE_PFA_WIDE : ECNF_NODE_PFA;
-};
-// waves / threads per workgroup of a kernel: Geo's, or ECNF_COLS_NW for the column-split team kernel
+constexpr int kColsNW = 8;
+// waves / threads per workgroup of a kernel: Geo's, or kColsNW for the column-split team kernel
 template <int NF, int NT, int P, bool COLS>
-constexpr int kernel_waves() { return COLS ? ECNF_COLS_NW : Geo<NF, NT, P>::NW; }
+constexpr int kernel_waves() { return COLS ? kColsNW : Geo<NF, NT, P>::NW; }
 template <int NF, int NT, int P, bool COLS>
 constexpr int kernel_threads() { return 64 * kernel_waves<NF, NT, P, COLS>(); }
 constexpr int kMaxBlocks = 10;
@@ -187,9 +147,6 @@ struct BlockW {
   // M = 256 tangent kernels: phi_e.0 kernel [(2H+1)][M] x -log2(e) as split node fragments (edge_layer1_dual)
   const unsigned* W1_s;
   float w1inv;
-  // fused-P split kernels (kFusedP): Wp_s / pinv hold -log2(e) x W_n W_p over the [h | temb] rows (K = H + T), so the
-  // phi_e.0 halves come straight from hin in the node-Dense phase; bnp_u = -log2(e) x (b_n W_p + [0 | b1])
-  const float* bnp_u;
   // the divergence kernels' chain: every chain layer scaled by a power of two and split into THREE fp16 pieces that
   // hold the fp32 weight exactly (chain_split WP = 3); 1 / the scales are cinv (the 2-piece chain Ws is unscaled and
   // ignores them with ECNF_CHAIN_BIAS_INIT, and uses the same scales without it)
@@ -396,48 +353,6 @@ __device__ __forceinline__ int opaque_u(int v) {
   return v;
 }
 
-// Halves mode (egnn_eval / integrate_kernel HALF): a 512-thread workgroup runs as two independent 256-thread halves
-// (waves 0-3 and 4-7; waves w and w + 4 share a SIMD), each with its own molecules, LDS region and solver, and
-// synchronised by its own LDS barrier instead of s_barrier, so one half's latency-bound node phases overlap the other
-// half's edge chains on the same SIMDs.  vtid: the thread index within the (half) workgroup.
-template <bool HALF>
-__device__ __forceinline__ int vtid() {
-  return HALF ? (opaque_tid() & 255) : opaque_tid();
-}
-
-// the barrier of a half: one monotonically increasing LDS arrival counter per half.  Lane 0 of each of the half's 4
-// waves adds 1; barrier n is complete when the counter reaches 4 (n + 1), i.e. 4 more than the multiple of 4 below the
-// value it read (no reset and no generation word, so no ordering between two stores is needed: an earlier form reset
-// the count and then bumped a generation with two relaxed stores, which are free to be reordered).  A wave cannot
-// arrive at barrier n + 1 before all 4 arrived at n, so the counts of consecutive barriers never mix.  The LDS writes
-// of each wave are complete (lgkmcnt(0)) before it arrives.  Never mixed with s_barrier after the kernel's start.
-__device__ __forceinline__ int* half_bar_words() {
-  __shared__ int bar[4];   // [half] arrival counters (2 used); zeroed at the kernel's start (integrate_kernel)
-  return bar;
-}
-__device__ __forceinline__ void half_barrier() {
-  int* bar = half_bar_words() + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 8));
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  int old = 0;
-  if ((threadIdx.x & 63) == 0) old = __hip_atomic_fetch_add(bar, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  const int target = (__builtin_amdgcn_readfirstlane(old) & ~3) + 4;
-  // bounded (seconds): a wave that never arrives would be a bug; the kernel then finishes with wrong results instead
-  // of hanging the device
-  for (unsigned spins = 0; (int)(__builtin_amdgcn_readfirstlane(__hip_atomic_load(bar, __ATOMIC_RELAXED,
-                                                                                   __HIP_MEMORY_SCOPE_WORKGROUP)) -
-                                 target) < 0 &&
-                           spins < (1u << 26);
-       ++spins)
-    __builtin_amdgcn_s_sleep(1);
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-}
-
-template <bool HALF>
-__device__ __forceinline__ void wg_sync() {
-  if constexpr (HALF) half_barrier();
-  else __syncthreads();
-}
-
 __device__ __forceinline__ f32x4 ldg4(const float* p, int idx4) { return gptr4(p)[idx4]; }
 
 __device__ __forceinline__ f32x16 mfma32(float a, float b, const f32x16& c) {
@@ -577,21 +492,12 @@ __device__ __forceinline__ void node_task(const float* X1, int ldx1, int K1, con
 // INPLACE (Y may alias X1): every wave of the workgroup calls it once (active = false: no task) and the outputs are
 // written after a barrier that follows every wave's k-loop.
 
-// the first ECNF_NODE_PFA k-steps of a node GEMM task's A fragments, loaded before the barrier that precedes the GEMM
-// (node_prefetch): the weights do not depend on the phase's inputs, so their L2 latency overlaps the barrier wait and
-// the previous phase's tail instead of opening every node phase
-struct NodePre {
-  u32x4 w[ECNF_NODE_PFA][2][kPieces];
-};
-
-template <int NA, int NT = 0, bool INPLACE = false, bool PRE = false, int PFA = ECNF_NODE_PFA>
+template <int NA, int NT = 0, bool INPLACE = false, int PFA = kNodePFADefault>
 __device__ __forceinline__ void node_task_split(const float* X1, int ldx1, int K1, const float* X2, int ldx2, int K2,
                                                 const unsigned* __restrict__ Wpk, float winv,
                                                 const float* __restrict__ bias, bool act, const float* resid, int ldr, float* Y, int ldy, int RP,
-                                                int nvalid, int jb, int ct, int lane, bool active = true,
-                                                const NodePre* pre = nullptr) {
-  // PFA: k-steps of A fragments in flight ahead of the MFMAs (the prefetched first k-steps of PRE are ECNF_NODE_PFA)
-  static_assert(!PRE || PFA == ECNF_NODE_PFA, "node_prefetch fills ECNF_NODE_PFA k-steps");
+                                                int nvalid, int jb, int ct, int lane, bool active = true) {
+  // PFA: k-steps of A fragments in flight ahead of the MFMAs
   jb = __builtin_amdgcn_readfirstlane(jb);   // uniform: buffer-load offsets in SGPRs (no waterfall loops)
   ct = __builtin_amdgcn_readfirstlane(ct);
   const int kk = lane >> 5, li = lane & 31;
@@ -657,17 +563,7 @@ __device__ __forceinline__ void node_task_split(const float* X1, int ldx1, int K
   if (active) {
   bload(0, n, bv);
   if constexpr (NT) bload(0, RP + n, bvT);
-  if constexpr (PRE) {
-    static_for<PFA>([&](auto Ic) {
-      constexpr int i = decltype(Ic)::value;
-#pragma unroll
-      for (int a = 0; a < NA; ++a)
-#pragma unroll
-        for (int p = 0; p < kPieces; ++p) wa[i][a][p] = pre->w[i][a][p];
-    });
-  } else {
-    static_for<PFA>([&](auto Ic) { aload(min((int)decltype(Ic)::value, nks - 1), wa[decltype(Ic)::value]); });
-  }
+  static_for<PFA>([&](auto Ic) { aload(min((int)decltype(Ic)::value, nks - 1), wa[decltype(Ic)::value]); });
   auto kstep = [&](int ks, auto Ic) {
     constexpr int i = decltype(Ic)::value;
     aload(min(ks + PFA, nks - 1), wa[(i + PFA) % S]);
@@ -740,84 +636,36 @@ __device__ __forceinline__ void node_task_split(const float* X1, int ldx1, int K
 // and get no bias, act'(pre) * (X_T W).  Output blocks are paired (shared B reads, two independent MFMA
 // chains) whenever the pairs still give every wave a task.
 // ---------------------------------------------------------------------------------------------------
-#ifndef ECNF_NODE_PAIR_DIV
-#define ECNF_NODE_PAIR_DIV 1
-#endif
 // split node GEMM task deal: two output blocks per task (sharing the B split) when the pairs still give every wave a
-// task
+// task (pairing at half / a quarter of the waves measured within noise, profiles/round3/ab)
 template <int NW>
 __device__ __forceinline__ bool node_paired(int njb, int nct) {
-  return (njb % 2) == 0 && (njb / 2) * nct >= NW / ECNF_NODE_PAIR_DIV;
+  return (njb % 2) == 0 && (njb / 2) * nct >= NW;
 }
 
-// issue the first PFA k-steps of A fragments of this wave's first task of the split node GEMM (node_gemm's deal) into
-// pre; no task: nothing.  The matching node_gemm<..., PRE = true> call consumes them.
-template <int NW>
-__device__ __forceinline__ void node_prefetch(const unsigned* __restrict__ Ws, int K1, int K2, int NOUT, int RP,
-                                              int wave, int lane, NodePre& pre) {
-  const int njb = NOUT >> 5, nct = RP >> 5;
-  const bool pair = node_paired<NW>(njb, nct);
-  const int ntask = pair ? (njb / 2) * nct : njb * nct;
-  if (wave >= ntask) return;
-  const int jb = __builtin_amdgcn_readfirstlane(pair ? 2 * (wave % (njb / 2)) : wave % njb);
-  const int nks = ((K1 + 15) >> 4) + ((K2 + 15) >> 4);
-  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned*>(Ws), (short)0,
-                                                                         0x7fffffff, 0x00020000);
-  static_for<ECNF_NODE_PFA>([&](auto Ic) {
-    constexpr int i = decltype(Ic)::value;
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-      if (a == 0 || pair)
-#pragma unroll
-        for (int p = 0; p < kPieces; ++p)
-          pre.w[i][a][p] = wload(rsrc, lane * 16, (((jb + a) * nks + min(i, nks - 1)) * kPieces + p) * kPieceBytes);
-  });
-}
-
-template <int NT, int NW, bool SPLIT, bool PRE = false, int PFA = ECNF_NODE_PFA>
+template <int NT, int NW, bool SPLIT, int PFA = kNodePFADefault>
 __device__ __forceinline__ void node_gemm(const float* X1, int ldx1, int K1, const float* X2, int ldx2, int K2,
                                           const float* __restrict__ W, const unsigned* __restrict__ Ws, float winv,
                                           int ldw, const float* __restrict__ bias, int NOUT, bool act, const float* resid,
-                                          int ldr, float* Y, int ldy, int RP, int nvalid, int wave, int lane,
-                                          const NodePre* pre = nullptr) {
+                                          int ldr, float* Y, int ldy, int RP, int nvalid, int wave, int lane) {
   const int njb = NOUT >> 5, nct = RP >> 5;
   if constexpr (SPLIT) {
     if (node_paired<NW>(njb, nct)) {   // two output blocks per task share the B split
       const int npair = njb / 2;
-      int task = wave;
-      if constexpr (PRE) {   // this wave's first task with its prefetched A fragments (node_prefetch)
-        if (task < npair * nct)
-          node_task_split<2, NT, false, true>(X1, ldx1, K1, X2, ldx2, K2, Ws, winv, bias, act, resid, ldr, Y, ldy, RP,
-                                              nvalid, 2 * (task % npair), task / npair, lane, true, pre);
-        task += NW;
-      }
-      for (; task < npair * nct; task += NW)
-        node_task_split<2, NT, false, false, PFA>(X1, ldx1, K1, X2, ldx2, K2, Ws, winv, bias, act, resid, ldr, Y, ldy, RP, nvalid,
-                               2 * (task % npair), task / npair, lane);
+      for (int task = wave; task < npair * nct; task += NW)
+        node_task_split<2, NT, false, PFA>(X1, ldx1, K1, X2, ldx2, K2, Ws, winv, bias, act, resid, ldr, Y, ldy, RP,
+                                           nvalid, 2 * (task % npair), task / npair, lane);
     } else {
-      int task = wave;
-      if constexpr (PRE) {
-        if (task < njb * nct)
-          node_task_split<1, NT, false, true>(X1, ldx1, K1, X2, ldx2, K2, Ws, winv, bias, act, resid, ldr, Y, ldy, RP,
-                                              nvalid, task % njb, task / njb, lane, true, pre);
-        task += NW;
-      }
-      for (; task < njb * nct; task += NW)
-        node_task_split<1, NT, false, false, PFA>(X1, ldx1, K1, X2, ldx2, K2, Ws, winv, bias, act, resid, ldr, Y, ldy, RP, nvalid,
-                               task % njb, task / njb, lane);
+      for (int task = wave; task < njb * nct; task += NW)
+        node_task_split<1, NT, false, PFA>(X1, ldx1, K1, X2, ldx2, K2, Ws, winv, bias, act, resid, ldr, Y, ldy, RP,
+                                           nvalid, task % njb, task / njb, lane);
     }
     return;
   }
-  if (false && (njb % 2) == 0 && (njb / 2) * nct >= NW) {   // pairing measured slower for phi_h (r01)
-    const int npair = njb / 2;
-    for (int task = wave; task < npair * nct; task += NW)
-      node_task<NT, 2>(X1, ldx1, K1, X2, ldx2, K2, W, ldw, bias, act, resid, ldr, Y, ldy, RP, nvalid,
-                       2 * (task % npair), task / npair, lane);
-  } else {
-    for (int task = wave; task < njb * nct; task += NW)
-      node_task<NT, 1>(X1, ldx1, K1, X2, ldx2, K2, W, ldw, bias, act, resid, ldr, Y, ldy, RP, nvalid,
-                       task % njb, task / njb, lane);
-  }
+  // the fp32 node GEMMs (strict-fp32 kernels): one output block per task (pairing measured slower for phi_h, r01)
+  for (int task = wave; task < njb * nct; task += NW)
+    node_task<NT, 1>(X1, ldx1, K1, X2, ldx2, K2, W, ldw, bias, act, resid, ldr, Y, ldy, RP, nvalid, task % njb,
+                     task / njb, lane);
 }
 
 // in-place split node GEMM (Y aliases X1; the M = 256 tangent kernels' phi_h on macc): output block pairs, at most one
@@ -880,9 +728,6 @@ __device__ __forceinline__ void node_gemm_inplace_f32(const float* X1, int ldx1,
 // layer, before group (0, NF-1) re-zeroes its accumulator and long before group (NF-1, *) reads it.  Only the
 // last layer's block NF-1 is left for a short tail.  sched_barriers pin this order and the weight prefetch
 // (PF groups ahead, contiguous across layers).
-#ifndef ECNF_EXP_PF
-#define ECNF_EXP_PF 2
-#endif
 template <int NF>
 struct ChainPlan {
   // SiLU work of group g (0..NF*NF-1) of a layer l: {block, layer offset (0 = this layer, -1 = previous), first
@@ -900,12 +745,7 @@ struct ChainPlan {
 template <int NT>
 __device__ __forceinline__ void chain_act(f32x16& x, f32x16& xt, const f32x16& a, const f32x16& at, int r, float b) {
   float y, yT = 0.f;
-#ifdef ECNF_EXP_NO_SILU
-  y = a[r] + b;
-  yT = NT ? at[r] : 0.f;
-#else
   silu_dual<NT>(a[r] + b, NT ? at[r] : 0.f, y, yT);
-#endif
   x[r] = y;
   if constexpr (NT) xt[r] = yT;
 }
@@ -916,7 +756,7 @@ __device__ __forceinline__ void chain_segment(f32x16 (&X)[NF], f32x16 (&XT)[NF],
   constexpr int GL = NF * NF;             // groups per layer, g = fb * NF + jb
   constexpr int G = NL * GL;
   constexpr int M = NF * 32;
-  constexpr int PF = ECNF_EXP_PF;         // groups in flight ahead of the MFMAs
+  constexpr int PF = 2;                   // groups in flight ahead of the MFMAs
   using Plan = ChainPlan<NF>;
   const int kk = lane >> 5;
   const gf32x4_p wp = gptr4(Wpk) + lane;
@@ -937,10 +777,8 @@ __device__ __forceinline__ void chain_segment(f32x16 (&X)[NF], f32x16 (&XT)[NF],
     constexpr int l = gg / GL, g = gg % GL, fb = g / NF, jb = g % NF;
     constexpr typename Plan::Task tk = Plan::task(g, l > 0);
     if constexpr (gg + PF < G) {
-#ifndef ECNF_EXP_NO_WLOAD
 #pragma unroll
       for (int q = 0; q < 4; ++q) wbuf[(gg + PF) % (PF + 1)][q] = wp[(gidx(gg + PF) + q) * 64];
-#endif
     }
     if constexpr (tk.j >= 0 && tk.e0 == 0) {
 #pragma unroll
@@ -983,7 +821,7 @@ __device__ __forceinline__ void chain_segment(f32x16 (&X)[NF], f32x16 (&XT)[NF],
 // Segmented (by receiver row) inclusive PREFIX sum over the 32 edge lanes of each half-wave, in DPP:
 // row_shr:1,2,4,8 inside each 16-lane row, then row_bcast:15 carries lane 15's running sum into lanes 16..31
 // (rows 1 and 3 only, so the two half-waves — same edges, different feature rows — never mix).  Each step is
-// v += ok_step * dpp(v): a mov_dpp and an fma per value, no LDS traffic and no waits.  Segments are contiguous
+// v += ok_step * dpp(v): one fused v_fmac_f32_dpp per value, no LDS traffic and no waits.  Segments are contiguous
 // lane runs, so "same segment as the source lane" is the Hillis-Steele condition; the tail lane of a segment
 // ends holding the segment's sum inside this tile.
 struct SegScan {
@@ -992,11 +830,6 @@ struct SegScan {
   template <int CTRL, int ROWMASK>
   __device__ __forceinline__ static int dpp_i(int v) {
     return __builtin_amdgcn_update_dpp(0, v, CTRL, ROWMASK, 0xF, true);
-  }
-  template <int CTRL, int ROWMASK>
-  __device__ __forceinline__ static float dpp_f(float v) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, ROWMASK, 0xF,
-                                                                  true));
   }
   __device__ __forceinline__ void init(int seg, int li) {
     const int sp = seg + 1;   // 0 marks "no source lane" (bound_ctrl / masked rows read 0)
@@ -1009,26 +842,16 @@ struct SegScan {
     const int nxt = __shfl_down(seg, 1, 32);
     tail = (li == 31) || (nxt != seg);
   }
-  // FUSED: the inline-asm form below (primal kernels); the builtin form otherwise
-  template <int NV, bool FUSED>
-  __device__ __forceinline__ void sum_many(float (&v)[NV]) const {
-#ifndef ECNF_DPP_BUILTIN
-    if constexpr (FUSED) {
-      sum_fused<NV>(v);
-      return;
-    }
-#endif
-    sum_builtin<NV>(v);
-  }
-  // one fused v_fmac_f32_dpp per value and step (v += ok * v[lane - shift]).  The builtin form compiles to
-  // v_mov_b32_dpp + v_fmac_f32 + s_nop 0 per value (the DPP read of a just-written temp needs wait states), 3 issue
-  // slots instead of 1.  Wait states for the fused form (the compiler's hazard recognizer does not look inside
+  // one fused v_fmac_f32_dpp per value and step (v += ok * v[lane - shift]).  The __builtin_amdgcn_update_dpp form
+  // compiles to v_mov_b32_dpp + v_fmac_f32 + s_nop 0 per value (the DPP read of a just-written temp needs wait
+  // states), 3 issue slots instead of 1.  Wait states for the fused form (the compiler's hazard recognizer does not look inside
   // inline asm): a value is re-read through DPP NV - 1 >= 2 instructions after its last write inside the scan, and
   // the s_nop 4 in front covers VALU writes of v (2 wait states) and an EXEC write just before the scan (5; e.g. the
-  // end of the tangent kernels' `if (writer)` stores).  Row masks as the builtin form (row_bcast:15 writes rows 1
-  // and 3 only; rows 0 and 2 keep v, where the builtin added ok * 0).
+  // end of the tangent kernels' `if (writer)` stores).  row_bcast:15 writes rows 1 and 3 only; rows 0 and 2 keep v.
+  // The consumers' wait states after the asm are checked on the built kernels (tools/isa_hazards.py,
+  // tests/test_isa_hazards.py).
   template <int NV>
-  __device__ __forceinline__ void sum_fused(float (&v)[NV]) const {
+  __device__ __forceinline__ void sum_many(float (&v)[NV]) const {
     static_assert(NV >= 3, "DPP wait states assume >= 3 interleaved values");
     // the scheduler must not sink the producers of v below the s_nop (volatile asm only orders asm statements)
     __builtin_amdgcn_sched_barrier(0);
@@ -1043,19 +866,6 @@ struct SegScan {
     ECNF_DPP_STEP(4, "row_bcast:15 row_mask:0xa")
 #undef ECNF_DPP_STEP
     __builtin_amdgcn_sched_barrier(0);
-  }
-  template <int NV>
-  __device__ __forceinline__ void sum_builtin(float (&v)[NV]) const {
-#pragma unroll
-    for (int i = 0; i < NV; ++i) v[i] = fmaf(okf[0], dpp_f<0x111, 0xF>(v[i]), v[i]);
-#pragma unroll
-    for (int i = 0; i < NV; ++i) v[i] = fmaf(okf[1], dpp_f<0x112, 0xF>(v[i]), v[i]);
-#pragma unroll
-    for (int i = 0; i < NV; ++i) v[i] = fmaf(okf[2], dpp_f<0x114, 0xF>(v[i]), v[i]);
-#pragma unroll
-    for (int i = 0; i < NV; ++i) v[i] = fmaf(okf[3], dpp_f<0x118, 0xF>(v[i]), v[i]);
-#pragma unroll
-    for (int i = 0; i < NV; ++i) v[i] = fmaf(okf[4], dpp_f<0x142, 0xA>(v[i]), v[i]);
   }
 };
 
@@ -1094,7 +904,7 @@ __device__ __forceinline__ void edge_shift(const Net& net, const BlockW& bw, con
     sh[d] = (phx * r[d]) / den;
     sh[D + d] = NT ? (phxT * r[d] + phx * dr[d]) / den - (phx * r[d]) * dlength / (den * den) : 0.f;
   }
-  sc.sum_many<2 * D, true>(sh);
+  sc.sum_many<2 * D>(sh);
   if (writer && kk == 0) {
 #pragma unroll
     for (int d = 0; d < D; ++d) {
@@ -1146,9 +956,7 @@ __device__ __forceinline__ void edge_tail(const Net& net, const BlockW& bw, cons
     float v[16];
 #pragma unroll
     for (int r16 = 0; r16 < 16; ++r16) v[r16] = m[fb][r16] * g;
-#ifndef ECNF_EXP_NO_AGG
-    sc.sum_many<16, true>(v);
-#endif
+    sc.sum_many<16>(v);
     if (writer && pw) {
       if (agg_dst) {
         // the segment part's sums as 4 x 16-B stores into its own row (no atomics; combined in the node update)
@@ -1171,7 +979,7 @@ __device__ __forceinline__ void edge_tail(const Net& net, const BlockW& bw, cons
     if constexpr (NT) {
 #pragma unroll
       for (int r16 = 0; r16 < 16; ++r16) v[r16] = gT * m[fb][r16] + g * mT[fb][r16];
-      sc.sum_many<16, true>(v);
+      sc.sum_many<16>(v);
       if (writer) {
         float* mrow = s.macc + (RP + rr) * s.ld_m + 4 * kk;
         asm volatile("" : "+v"(mrow));
@@ -1184,9 +992,7 @@ __device__ __forceinline__ void edge_tail(const Net& net, const BlockW& bw, cons
 
   // phi_x torso (egnn.py:82) then its Dense(1) and the shifts
   phi_x(X, XT);
-#ifndef ECNF_EXP_NO_SHIFT
   edge_shift<NF, NT, L, D>(net, bw, s, X, XT, writer, sc, rr, r, dr, length, dlength, lane, pw);
-#endif
 }
 
 // M = 256 tangent kernels: phi_e.0 on the edge itself, [h_s | h_r | |r|^2] W1 + b1 (egnn.py:76-79; no per-node P
@@ -1336,10 +1142,7 @@ __device__ __forceinline__ void edge_layer1_dual_f32(const Net& net, const Block
 // block), the fp32 fragments of chain_segment ([layer][jb][fb][q][lane][4]) streamed PF groups ahead
 template <int NF>
 __device__ __forceinline__ void dual_pass_f32(const f32x16 (&X)[NF], f32x16 (&acc)[NF], gf32x4_p wl) {
-#ifndef ECNF_W32_PF
-#define ECNF_W32_PF 2
-#endif
-  constexpr int G = NF * NF, PF = ECNF_W32_PF;
+  constexpr int G = NF * NF, PF = 2;
   f32x4 wbuf[PF + 1][4];
   static_for<PF>([&](auto Gc) {
     constexpr int gg = decltype(Gc)::value;
@@ -1409,25 +1212,6 @@ template <int NF, int NT, int L, int D, int P, int WPP = kPieces>
 __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, const Lds& s, int tile, int lane, bool agg,
                                           int a = -1, int part = 0, int amode = 1) {
   const int kk = lane >> 5, li = lane & 31;
-#ifdef ECNF_EXP_CHAIN_ONLY
-  {  // timing experiment: the two chain segments alone, on synthetic activations, one LDS add as the sink
-    f32x16 X[NF], XT[NF];
-#pragma unroll
-    for (int fb = 0; fb < NF; ++fb)
-#pragma unroll
-      for (int r16 = 0; r16 < 16; ++r16) X[fb][r16] = 0.01f * (fb * 16 + r16) + 1e-3f * lane + 1e-4f * tile;
-    chain_segment<NF, NT, L - 1>(X, XT, launder_uniform(bw.We), s.vecs, lane);
-    chain_segment<NF, NT, L>(X, XT, launder_uniform(bw.We + (L - 1) * NF * NF * 1024), s.vecs + (L - 1) * NF * 32,
-                             lane);
-    float acc = 0.f;
-#pragma unroll
-    for (int fb = 0; fb < NF; ++fb)
-#pragma unroll
-      for (int r16 = 0; r16 < 16; ++r16) acc += X[fb][r16];
-    lds_add(&s.dxacc[li], acc);
-    return;
-  }
-#endif
   const int N = net.N, nn1 = N - 1, RP = net.RP, M = NF * 32;
   int mol, i, sd;
   bool valid;
@@ -1678,11 +1462,7 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
 #pragma unroll
       for (int e4 = 0; e4 < 4; ++e4) {
         const int row = fb * 32 + 8 * q + 4 * kk + e4;
-#ifdef ECNF_EXP_NO_L1GATHER
-        const float p = 0.01f * row + len2 * w[e4];
-#else
         const float p = Ps[row] + Pr[row] + len2 * w[e4];
-#endif
         float y, yT = 0.f;
         if constexpr (NT) {
           const float pT = PsT[row] + PrT[row] + dlen2 * w[e4];
@@ -1727,9 +1507,9 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
 }
 
 // ---------------------------------------------------------------------------------------------------
-// Column-split team mode (team cols; the M = 256 split primal kernels, ECNF_COLS_NW = 8 waves): every member
+// Column-split team mode (team cols; the M = 256 split primal kernels, kColsNW = 8 waves): every member
 // workgroup of a molecule's team runs ONE edge tile per block, and its waves split each chain layer of that tile by
-// output block (wave w: blocks [w NJ, (w + 1) NJ), NJ = NF / ECNF_COLS_NW), exchanging the layer through an LDS image (Lds::xs): split pieces
+// output block (wave w: blocks [w NJ, (w + 1) NJ), NJ = NF / kColsNW), exchanging the layer through an LDS image (Lds::xs): split pieces
 // in the MFMA B-operand layout between layers, fp32 after a segment's last layer.  Per output element the arithmetic
 // is chain_split's (the same MFMA sequence from the bias column, the same log2-domain SiLU, pair split and fp32 last
 // layer), and the gate / phi_x-output dot products read the whole fp32 layer back and sum in the batch order
@@ -1818,21 +1598,19 @@ __device__ __forceinline__ void cols_act(f32x16 (&acc)[NJ], float* xs, int j0, i
   });
 }
 
-#ifndef ECNF_COLS_PF
-#define ECNF_COLS_PF 8   // weight groups in flight per wave in the column-split chain (its fragments come from L2)
-#endif
+constexpr int kColsPF = 8;   // weight groups in flight per wave in the column-split chain (its fragments come from L2)
 // NL chained layers on the tile, the waves split by output block (wave w: blocks j0 .. j0 + NJ - 1, j0 = w NJ).
 // Input: the full split layer X (registers; also in the image); output: the last layer's fp32 activations of EVERY
 // block in m (read back from the image).  Per layer and block the MFMA sequence of chain_split (kBI: C = the bias
 // column, then the k-steps (fb, u) in order, three cross terms each, smallest first) and its activation; two
 // workgroup barriers per layer (after the MFMAs: every wave has read the image; after the stores).  The wave's
 // weight groups (chain_split's packed layout: [layer][jb][fb][u][piece], 1 KiB per piece) stream as ONE sequence over
-// the layers, ECNF_COLS_PF groups ahead, so the next layer's first fragments are in flight across the barriers and
+// the layers, kColsPF groups ahead, so the next layer's first fragments are in flight across the barriers and
 // the activation (each wave reads its own blocks' fragments from L2: nothing is shared in L1 as in the batch path).
 template <int NF, int NL>
 __device__ __forceinline__ void cols_segment(SplitX<NF>& X, f32x16 (&m)[NF], const unsigned* __restrict__ W,
                                              const float* bias, float* xs, int wave, int lane) {
-  constexpr int NJ = NF / ECNF_COLS_NW, GB = 2 * NF, GL = GB * NF, NG = NJ * GB, NQ = NL * NG, PF = ECNF_COLS_PF;
+  constexpr int NJ = NF / kColsNW, GB = 2 * NF, GL = GB * NF, NG = NJ * GB, NQ = NL * NG, PF = kColsPF;
   const int j0 = wave * NJ, kk = lane >> 5;
   const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned*>(W), (short)0,
                                                                          0x7fffffff, 0x00020000);
@@ -1861,7 +1639,7 @@ __device__ __forceinline__ void cols_segment(SplitX<NF>& X, f32x16 (&m)[NF], con
           acc[j][4 * r4 + 3] = b4[3];
         });
       });
-      __builtin_amdgcn_s_setprio(ECNF_CHAIN_PRIO);
+      __builtin_amdgcn_s_setprio(kChainPrio);
     }
     if constexpr (q + PF < NQ) {
 #pragma unroll
@@ -1895,8 +1673,8 @@ __device__ __forceinline__ void cols_segment(SplitX<NF>& X, f32x16 (&m)[NF], con
 template <int NF, int L, int D>
 __device__ __forceinline__ void edge_tile_cols(const Net& net, const BlockW& bw, const Lds& s, int tile, int wave,
                                                int lane, bool agg) {
-  static_assert(NF % ECNF_COLS_NW == 0, "cols mode deals the output blocks over the workgroup's waves");
-  constexpr int NJ = NF / ECNF_COLS_NW, M = NF * 32;
+  static_assert(NF % kColsNW == 0, "cols mode deals the output blocks over the workgroup's waves");
+  constexpr int NJ = NF / kColsNW, M = NF * 32;
   const int kk = lane >> 5, li = lane & 31, j0 = wave * NJ;
   const int N = net.N, nn1 = N - 1;
   const int mol = (tile * 32) / net.EP;
@@ -1990,7 +1768,7 @@ __device__ __forceinline__ void edge_tile_cols(const Net& net, const BlockW& bw,
         float v[16];
 #pragma unroll
         for (int r16 = 0; r16 < 16; ++r16) v[r16] = m[fb][r16] * g;
-        sc.sum_many<16, true>(v);
+        sc.sum_many<16>(v);
         if (writer) {
           if (agg_dst) {
 #pragma unroll
@@ -2093,16 +1871,20 @@ __device__ __forceinline__ void team_exchange(const Net& net, const Lds& s, cons
     st16(off_d + 4 * idx, *reinterpret_cast<const f32x4*>(s.dxacc + 4 * idx));
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains its write-through stores
   __syncthreads();
-  // ---- arrive, then wait for the whole team
+  // ---- arrive, then wait for the whole team.  A timeout is sticky: once any member has flagged the molecule (a member
+  // not running), every later wait of every member sees the flag at its first poll (and every 256th after) and gives
+  // up at once, so a broken team costs one poll budget, not one per exchange.
   if (tid == 0) {
     gu32_p ctr = (gu32_p)(tm.p.ctr + tm.T);
+    ECNF_GLOBAL int* tflag = (ECNF_GLOBAL int*)(tm.p.timeout + tm.T);
     __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned want = (unsigned)G * (unsigned)(epoch + 1);
     unsigned spins = 0;
     while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
+      if ((spins & 255u) == 0 && __hip_atomic_load(tflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
       __builtin_amdgcn_s_sleep(2);
       if (++spins > (1u << 24)) {   // seconds: a member is not running (not co-resident); give up, flag it
-        __hip_atomic_store((ECNF_GLOBAL int*)(tm.p.timeout + tm.T), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(tflag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
     }
@@ -2164,26 +1946,20 @@ __device__ __forceinline__ void team_exchange(const Net& net, const Lds& s, cons
 // one full evaluation.  x_in/tan_in/v_out/tan_out: LDS [MPW][N*D]; t_in: LDS [MPW] (actual time).
 // Must be called by all Geo<NF, NT, P>::NTHR threads of the workgroup (NW waves); returns after a barrier.
 // ---------------------------------------------------------------------------------------------------
-template <int NF, int NT, int L, int D, int P, bool TEAM = false, bool HALF = false, bool COLS = false>
+template <int NF, int NT, int L, int D, int P, bool TEAM = false, bool COLS = false>
 __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const float* x_in, const float* t_in, const float* tan_in,
                           float* v_out, float* tan_out, const int* act = nullptr, int sparse_a = -1,
                           float* pcache = nullptr, int pmode = 0, const TeamCtx* tm = nullptr,
                           int* tepoch = nullptr) {
-  constexpr int kNW = HALF ? 4 : kernel_waves<NF, NT, P, COLS>(), kNT = HALF ? 256 : kernel_threads<NF, NT, P, COLS>();
+  constexpr int kNW = kernel_waves<NF, NT, P, COLS>(), kNT = kernel_threads<NF, NT, P, COLS>();
   constexpr bool kSplitG = Geo<NF, NT, P>::kSplit;
   constexpr bool kSplitN = Geo<NF, NT, P>::kSplitN;   // split node GEMMs (primal split kernels and tangent kernels)
-#ifndef ECNF_NODE_PREFETCH
-#define ECNF_NODE_PREFETCH 0
-#endif
-  // node-GEMM A fragments prefetched across the barrier in front of each node GEMM (node_prefetch): the split primal
-  // kernels (M <= 128; the M = 256 primal kernels need their registers)
-  constexpr bool kPre = ECNF_NODE_PREFETCH && kSplitG && !Geo<NF, NT, P>::kFusedP && NF <= 4;
   // the exact trace's sparse blocks (primal + dual tiles, see the edge loop) in the M <= 128 split tangent kernels;
   // not compiled for the L = 2 shapes (M, D) = (128, 3), (64, 2), where the primal tile's code beside the dual
   // tile's spilled 36 B per lane (tests/test_kernel_resources.py).  The BASELINE shapes (LJ13 128/3/3, ALDP 64/2/3,
   // DW4 128/3/2) have it.
   constexpr bool kSparseX = Geo<NF, NT, P>::kL2T && !(L == 2 && (NF == 4 || D == 2));
-  const int tid = vtid<HALF>(), lane = tid & 63;
+  const int tid = opaque_tid(), lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: task indices stay in SGPRs
   const int N = net.N, H = net.H, T = net.T, M = NF * 32, RP = net.RP, MPW = net.MPW, ND = net.ND;
   const int nvalid = MPW * N;
@@ -2205,7 +1981,7 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
     const float arg = ts * net.freqs[k < half ? k : k - half];
     s.temb[idx] = k < half ? sinf(arg) : cosf(arg);
   }
-  wg_sync<HALF>();
+  __syncthreads();
   for (int idx = tid, VD = opaque_u(nvalid * D), No = opaque_u(N); idx < VD * (1 + NT); idx += kNT) {
     const int which = idx / VD, nd = idx - which * VD, n = nd / D, d = nd - n * D;
     const int m = n / No;
@@ -2223,7 +1999,7 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
     }
     s.hin[row * s.ld_hin + c] = v;
   }
-  wg_sync<HALF>();
+  __syncthreads();
   STAMP(s, kStPrologue);
 
   const int ntiles = (MPW * net.EP) >> 5;
@@ -2231,13 +2007,9 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
     const BlockW& bw = net.blk[k];
     // fresh (opaque) thread indices per phase group: per-thread addresses of the node phases are then computed after
     // the edge phase instead of being hoisted above it and kept live (spilled) through it
-    int tid = vtid<HALF>(), lane = tid & 63;
+    int tid = opaque_tid(), lane = tid & 63;
     // the last block's h update (gate, aggregation, phi_h) is dead: the field is x_K - x_c - mean (egnn.py:176-188)
     const bool need_h = k + 1 < net.K;
-    // split primal kernels: each node GEMM's first A fragments are loaded before the barrier in front of it
-    // (node_prefetch; -DECNF_NODE_PREFETCH=0 builds the A/B form without)
-    NodePre pre;
-    if constexpr (kPre) node_prefetch<kNW>(bw.Wn_s, H + T, 0, H, RP, wave, lane, pre);
     // stage this block's chain biases and the w_d / w_g / w_x vectors in LDS (read by every edge tile)
     {
       const float* be = (kSplitG || Geo<NF, NT, P>::kSplitT || Geo<NF, NT, P>::kWideT) ? bw.be_u : bw.be;
@@ -2255,52 +2027,28 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
       }
     }
     // h <- Dense([h | temb])  (egnn.py:166-167)
-    if constexpr (Geo<NF, NT, P>::kFusedP) {
-      // ... and, in the same phase, the per-node phi_e.0 halves P = [h | temb] (W_n W_p) + (b_n W_p + [0 | b1]) in
-      // the log2 domain (host-fused weights), with the Dense tasks dealt from the other end of the waves
-      node_gemm<NT, kNW, true>(s.hin, s.ld_hin, H + T, nullptr, 0, 0, bw.Wn, bw.Wn_s, bw.ninv, H, bw.bn, H, false,
-                               nullptr, 0, s.hb, s.ld_hb, RP, nvalid, kNW - 1 - wave, lane);
-      node_gemm<NT, kNW, true>(s.hin, s.ld_hin, H + T, nullptr, 0, 0, bw.Wp, bw.Wp_s, bw.pinv, 2 * M, bw.bnp_u, 2 * M,
-                               false, nullptr, 0, s.P, s.ld_P, RP, nvalid, wave, lane);
-      wg_sync<HALF>();
-      STAMP(s, kStNodeDense);
-    } else {
-    node_gemm<NT, kNW, kSplitN, kPre, Geo<NF, NT, P>::kNodePFA>(s.hin, s.ld_hin, H + T, nullptr, 0, 0, bw.Wn, bw.Wn_s, bw.ninv, H, bw.bn, H,
-                                      false, nullptr, 0, s.hb, s.ld_hb, RP, nvalid, wave, lane, &pre);
-    if constexpr (kPre && !Geo<NF, NT, P>::kNoP) node_prefetch<kNW>(bw.Wp_s, H, 0, 2 * M, RP, wave, lane, pre);
-    wg_sync<HALF>();
+    node_gemm<NT, kNW, kSplitN, Geo<NF, NT, P>::kNodePFA>(s.hin, s.ld_hin, H + T, nullptr, 0, 0, bw.Wn, bw.Wn_s, bw.ninv, H, bw.bn, H,
+                                      false, nullptr, 0, s.hb, s.ld_hb, RP, nvalid, wave, lane);
+    __syncthreads();
     STAMP(s, kStNodeDense);
     // per-node halves of phi_e layer 1 (the M = 256 tangent kernels compute layer 1 per edge)
     if constexpr (!Geo<NF, NT, P>::kNoP) {
       constexpr bool kPu = kSplitG || Geo<NF, NT, P>::kL2T;   // log2-domain P
-      node_gemm<NT, kNW, kSplitN, kPre, Geo<NF, NT, P>::kNodePFA>(s.hb, s.ld_hb, H, nullptr, 0, 0, bw.Wp, bw.Wp_s, bw.pinv, 2 * M,
+      node_gemm<NT, kNW, kSplitN, Geo<NF, NT, P>::kNodePFA>(s.hb, s.ld_hb, H, nullptr, 0, 0, bw.Wp, bw.Wp_s, bw.pinv, 2 * M,
                                         kPu ? bw.bp_u : bw.bp, 2 * M, false, nullptr, 0, s.P, s.ld_P, RP, nvalid, wave,
-                                        lane, &pre);
-      wg_sync<HALF>();
+                                        lane);
+      __syncthreads();
     }
-    }   // !kFusedP
     STAMP(s, kStPGemm);
     // edges
     // tile t runs on wave t mod NW, i.e. SIMD t mod 4: every SIMD gets ceil/floor(ntiles / 4) tiles
-#ifdef ECNF_EXP_BALANCED
-    // timing experiment: every wave runs the same number of tiles (padding tiles are invalid)
-    const int ntiles_run = ((ntiles + kNW - 1) / kNW) * kNW;
-#else
-    const int ntiles_run = ntiles;
-#endif
-#ifdef ECNF_EXP_BALANCED
-    {
-      const int elane = vtid<HALF>() & 63;
-      for (int tile = wave; tile < ntiles_run; tile += kNW) edge_tile<NF, NT, L, D, P>(net, bw, s, tile, elane, need_h);
-    }
-#else
     {
       // act (LDS [MPW], the solver's per-molecule flags; nullptr = every slot): the edge tiles of molecules whose
       // adaptive solve has finished, and of slots that pad the last workgroup, are skipped and the remaining tiles
       // are dealt round-robin over the waves, so a workgroup's tail after its faster molecules finish runs at the
       // cost of the molecules still integrating.  Skipped molecules' outputs are never committed; every molecule's
       // tiles and node rows are its own, so the others' results are unchanged (bitwise).
-      const int elane = vtid<HALF>() & 63;
+      const int elane = opaque_tid() & 63;
       const int tpm = net.EP >> 5;
       unsigned amask = MPW >= 32 ? 0xffffffffu : (1u << MPW) - 1u;
       if (act) {
@@ -2308,7 +2056,6 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
         for (int m = 0; m < MPW; ++m) amask |= (act[m] != 0 ? 1u : 0u) << m;
       }
       amask = __builtin_amdgcn_readfirstlane(amask);
-      (void)ntiles_run;
       const int nact = __builtin_popcount(amask);
       auto nth_active = [&](int q) {
         unsigned mm = amask;
@@ -2355,10 +2102,7 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
           edge_tile_cols<NF, L, D>(net, bw, s, nth_active(q) * tpm + (vt - q * tpm), wave, elane, need_h);
         }
       } else {
-      // halves mode: the second half deals its tiles from the last wave down, so the SIMD partners w and w + 4 of
-      // the two halves (3, 3, 2, 2 tiles each at 10 tiles) carry 5 tiles per SIMD between them
-      const int dwave = HALF && (threadIdx.x >> 8) ? kNW - 1 - wave : wave;
-      for (int vt = tfirst + dwave * tstep; vt < nrun; vt += kNW * tstep) {
+      for (int vt = tfirst + wave * tstep; vt < nrun; vt += kNW * tstep) {
         if constexpr (kSparseX) {
           if (vt < nd) {
             const int q = vt / ndt;
@@ -2378,11 +2122,7 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
       }
       }   // !COLS
     }
-#endif
-    constexpr bool kHu0 = kSplitG || Geo<NF, NT, P>::kL2T;   // log2-domain messages, scale in phi_h.0
-    if constexpr (kPre)
-      if (need_h) node_prefetch<kNW>(kHu0 ? bw.Wh_s[0] : bw.Wh_sn0, M, H, M, RP, wave, vtid<HALF>() & 63, pre);
-    wg_sync<HALF>();
+    __syncthreads();
     if constexpr (TEAM) {   // team mode: rebuild the molecule's aggregates from every member's tiles
       STAMP(s, kStEdge);
       team_exchange<NT, kNT>(net, s, *tm, *tepoch);
@@ -2402,11 +2142,11 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
           const int m = idx / (N * D);
           pcache[m * pstride + N * M + (k == 0 ? 0 : N * D) + (idx - m * N * D)] = s.dxacc[idx];
         }
-        wg_sync<HALF>();
+        __syncthreads();
       }
     }
     STAMP(s, kStEdge);
-    tid = vtid<HALF>();
+    tid = opaque_tid();
     lane = tid & 63;
     // node update: x += shift_i / (N-1) (egnn.py:95,113); m_i /= sqrt(N-1) (egnn.py:104)
     for (int idx = tid; idx < R * D; idx += kNT) {
@@ -2414,7 +2154,7 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
       s.dxacc[idx] = 0.f;
     }
     if (!need_h) {   // last block: no h update
-      wg_sync<HALF>();
+      __syncthreads();
       STAMP(s, kStNodeUpd);
       continue;
     }
@@ -2437,7 +2177,7 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
         s.macc[row * s.ld_m + c] = s.macc[row * s.ld_m + c] / net.sqrt_nn1;
       }
     }
-    wg_sync<HALF>();
+    __syncthreads();
     if constexpr (kSplitG) {
       if (net.cross) {   // the cross buffer overlaid hin's time-embedding columns: restore them
         for (int idx = tid; idx < nvalid * T; idx += kNT) {
@@ -2452,51 +2192,50 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
       // in place on macc (no P region in these kernels), then macc restarts from +0 for the next block's aggregates
       node_gemm_inplace<NT, kNW>(s.macc, s.ld_m, M, s.hb, s.ld_hb, H, bw.Wh_sn0, bw.hinv_n0, bw.bh[0], M, true,
                                  s.macc, s.ld_m, RP, nvalid, wave, lane);
-      wg_sync<HALF>();
+      __syncthreads();
       for (int l = 1; l < L; ++l) {
         node_gemm_inplace<NT, kNW>(s.macc, s.ld_m, M, nullptr, 0, 0, bw.Wh_s[l], bw.hinv[l], bw.bh[l], M, true, s.macc,
                                    s.ld_m, RP, nvalid, wave, lane);
-        wg_sync<HALF>();
+        __syncthreads();
       }
       node_gemm<NT, kNW, true>(s.macc, s.ld_m, M, nullptr, 0, 0, bw.Wh[L], bw.Wh_s[L], bw.hinv[L], H, bw.bh[L], H, false,
                                s.hb, s.ld_hb, s.hin, s.ld_hin, RP, nvalid, wave, lane);
-      wg_sync<HALF>();
+      __syncthreads();
       for (int idx = tid; idx < R * M; idx += kNT) {
         const int row = idx / M, c = idx - row * M;
         s.macc[row * s.ld_m + c] = 0.f;
       }
-      wg_sync<HALF>();
+      __syncthreads();
       STAMP(s, kStPhiH);
       continue;
     }
     if constexpr (Geo<NF, NT, P>::kWideT32) {   // the same in fp32 (macc already carries the 1 / sqrt(N - 1))
       node_gemm_inplace_f32<NT, kNW>(s.macc, s.ld_m, M, s.hb, s.ld_hb, H, bw.Wh[0], M, bw.bh[0], M, true, s.macc,
                                      s.ld_m, RP, nvalid, wave, lane);
-      wg_sync<HALF>();
+      __syncthreads();
       for (int l = 1; l < L; ++l) {
         node_gemm_inplace_f32<NT, kNW>(s.macc, s.ld_m, M, nullptr, 0, 0, bw.Wh[l], M, bw.bh[l], M, true, s.macc,
                                        s.ld_m, RP, nvalid, wave, lane);
-        wg_sync<HALF>();
+        __syncthreads();
       }
       node_gemm<NT, kNW, false>(s.macc, s.ld_m, M, nullptr, 0, 0, bw.Wh[L], nullptr, 1.0f, H, bw.bh[L], H, false,
                                 s.hb, s.ld_hb, s.hin, s.ld_hin, RP, nvalid, wave, lane);
-      wg_sync<HALF>();
+      __syncthreads();
       for (int idx = tid; idx < R * M; idx += kNT) {
         const int row = idx / M, c = idx - row * M;
         s.macc[row * s.ld_m + c] = 0.f;
       }
-      wg_sync<HALF>();
+      __syncthreads();
       STAMP(s, kStPhiH);
       continue;
     }
     float* Q0 = s.P;
     float* Q1 = s.P + (kSplitN ? M + 4 : M + 1);   // 16-B aligned rows for the split node GEMMs
     constexpr bool kHu = kSplitG || Geo<NF, NT, P>::kL2T;   // log2-domain messages, scale in phi_h.0
-    node_gemm<NT, kNW, kSplitN, kPre, Geo<NF, NT, P>::kNodePFA>(s.macc, s.ld_m, M, s.hb, s.ld_hb, H, bw.Wh[0], kHu ? bw.Wh_s[0] : bw.Wh_sn0,
+    node_gemm<NT, kNW, kSplitN, Geo<NF, NT, P>::kNodePFA>(s.macc, s.ld_m, M, s.hb, s.ld_hb, H, bw.Wh[0], kHu ? bw.Wh_s[0] : bw.Wh_sn0,
                                       kHu ? bw.hinv[0] : bw.hinv_n0, M, bw.bh[0], M, true, nullptr, 0, Q0, s.ld_P, RP,
-                                      nvalid, wave, lane, &pre);
-    if constexpr (kPre) node_prefetch<kNW>(bw.Wh_s[1], M, 0, L == 1 ? H : M, RP, wave, lane, pre);
-    wg_sync<HALF>();
+                                      nvalid, wave, lane);
+    __syncthreads();
     if (!(kSplitG && net.cross)) {   // atomically accumulated aggregates restart from +0
       for (int idx = tid; idx < R * M; idx += kNT) {
         const int row = idx / M, c = idx - row * M;
@@ -2504,15 +2243,14 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
       }
     }
     for (int l = 1; l < L; ++l) {
-      node_gemm<NT, kNW, kSplitN, kPre, Geo<NF, NT, P>::kNodePFA>(Q0, s.ld_P, M, nullptr, 0, 0, bw.Wh[l], bw.Wh_s[l], bw.hinv[l], M, bw.bh[l], M,
-                                        true, nullptr, 0, Q1, s.ld_P, RP, nvalid, wave, lane, &pre);
-      if constexpr (kPre) node_prefetch<kNW>(bw.Wh_s[l + 1], M, 0, l + 1 == L ? H : M, RP, wave, lane, pre);
-      wg_sync<HALF>();
+      node_gemm<NT, kNW, kSplitN, Geo<NF, NT, P>::kNodePFA>(Q0, s.ld_P, M, nullptr, 0, 0, bw.Wh[l], bw.Wh_s[l], bw.hinv[l], M, bw.bh[l], M,
+                                        true, nullptr, 0, Q1, s.ld_P, RP, nvalid, wave, lane);
+      __syncthreads();
       float* tq = Q0; Q0 = Q1; Q1 = tq;
     }
-    node_gemm<NT, kNW, kSplitN, kPre, Geo<NF, NT, P>::kNodePFA>(Q0, s.ld_P, M, nullptr, 0, 0, bw.Wh[L], bw.Wh_s[L], bw.hinv[L], H, bw.bh[L], H,
-                                      false, s.hb, s.ld_hb, s.hin, s.ld_hin, RP, nvalid, wave, lane, &pre);
-    wg_sync<HALF>();
+    node_gemm<NT, kNW, kSplitN, Geo<NF, NT, P>::kNodePFA>(Q0, s.ld_P, M, nullptr, 0, 0, bw.Wh[L], bw.Wh_s[L], bw.hinv[L], H, bw.bh[L], H,
+                                      false, s.hb, s.ld_hb, s.hin, s.ld_hin, RP, nvalid, wave, lane);
+    __syncthreads();
     STAMP(s, kStPhiH);
   }
 
@@ -2529,7 +2267,7 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
     float* dst = which == 0 ? v_out : tan_out;
     dst[m * ND + (n - m * N) * D + d] = v;
   }
-  wg_sync<HALF>();
+  __syncthreads();
   STAMP(s, kStEpilogue);
 }
 

@@ -175,11 +175,10 @@ int ecnf_molecules_per_workgroup(ecnf_handle* h, int32_t with_tangent, int32_t* 
 /* Arithmetic of the edge-MLP chain GEMMs (the bulk of the FLOPs) in this handle's kernels at its current precision
  * (diagnostic):
  *   ECNF_CHAIN_FP32_MFMA   v_mfma_f32_32x32x2_f32, fp32 operands
- *   ECNF_CHAIN_SPLIT_BF16  fp32 operands split into three bf16 pieces (RNE), the six cross terms above 2^-25 of
- *                          the product on v_mfma_f32_32x32x16_bf16, fp32 accumulation (fp32-accurate)
- *   ECNF_CHAIN_SPLIT_F16   fp32 operands split into two fp16 pieces (RNE; weights scaled by a power of two per
- *                          matrix), the three cross terms above 2^-21 of the product on v_mfma_f32_32x32x16_f16,
- *                          fp32 accumulation (the default build) */
+ *   ECNF_CHAIN_SPLIT_BF16  (reserved: the round-1 three-piece bf16 form, no longer built)
+ *   ECNF_CHAIN_SPLIT_F16   fp32 operands split into two fp16 pieces (RNE; node-GEMM weights scaled by a power of two
+ *                          per matrix), the three cross terms above 2^-21 of the product on v_mfma_f32_32x32x16_f16,
+ *                          fp32 accumulation */
 #define ECNF_CHAIN_FP32_MFMA 0
 #define ECNF_CHAIN_SPLIT_BF16 1
 #define ECNF_CHAIN_SPLIT_F16 2

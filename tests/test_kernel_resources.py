@@ -39,7 +39,7 @@ def test_split_kernels_do_not_spill():
     for kind, nf, nt, l, d, p, scratch in ks:
         if p != 0:
             continue   # the strict-fp32 comparator kernels (8 waves of fp32 MFMA chains) are not budgeted here
-        # Round 4: every split-precision integrate kernel (batch, team and halves modes, primal and tangent, every M)
+        # Round 4: every split-precision integrate kernel (batch and team modes, primal and tangent, every M)
         # runs without scratch; the loop-invariant values that used to spill (division constants of runtime sizes,
         # the solver's sizes and control flags, the aggregation's lane addresses) are re-derived at their use sites
         # (opaque_u / solver_size / an opaque row offset).  vf_kernel (one evaluation, not the solve loop): the M = 64
