@@ -290,7 +290,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    # under torch.distributed.run the process group forms at every world size (one rank included: the eval leg's
+    # reductions then run through RCCL, tests/test_gpu_rccl.py); a plain `python bench.py` run has no group
+    if "WORLD_SIZE" in os.environ:
         ndev = max(1, torch.cuda.device_count())
         local = local % ndev                  # one rank per GPU; folds ranks onto fewer GPUs only in rehearsals
         torch.cuda.set_device(local)
@@ -531,7 +533,8 @@ def main():
             "config": {"workload": f"{args.config} sample, Euler NFE={nfe_seen}, global batch {G} "
                                    f"({B} per GPU on rank 0)",
                        "n_nodes": cfg.n_nodes, "batch_per_gpu": B, "global_batch": G,
-                       "nfe": nfe_seen, "solver": "euler", "parallelism": f"dp{world}"},
+                       "nfe": nfe_seen, "solver": "euler", "parallelism": f"dp{world}",
+                       "dist_backend": dist.get_backend() if dist.is_initialized() else None},
             "matmul": {"gemms": chain_mode, "tangent_kernels": h.chain_arithmetic(True) + " edge chains",
                        "accumulate": "f32", "strict_fp32": fp32},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
@@ -556,7 +559,7 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

@@ -41,7 +41,8 @@ def global_normal(n_total: int, event_dim: int, seed: int, lo: int, hi: int, dev
 
 
 def _allreduce(t: torch.Tensor, op) -> torch.Tensor:
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+    # every initialised group reduces, one rank included (an identity, but the RCCL path then runs on one GPU)
+    if dist.is_available() and dist.is_initialized():
         if t.is_cuda and dist.get_backend() == "gloo":
             # gloo rehearsals (tests, several ranks folded onto one GPU): reduce a host copy
             h = t.cpu()
