@@ -399,9 +399,13 @@ bool split_primal(const ecnf_cfg& c, int NT, int P) {
   return kSplitChain && P == 0 && !NT && c.mlp_width <= 32 * kSplitMaxNF;
 }
 
-// Geo<NF, 1, P>::kWideT / kWideT32: the M = 256 tangent kernels at either precision (per-edge phi_e.0, no P rows in
-// LDS, in-place phi_h for one 32-row node tile)
-bool wide_tangent(const ecnf_cfg& c, int NT, int P) { (void)P; return NT && c.mlp_width == 256; }
+// Geo<NF, 1, P, BN>::kWideT / kWideT32: the tangent kernels in the wide form at either precision (per-edge phi_e.0,
+// no P rows in LDS, in-place phi_h): every M = 256 tangent kernel, and the M = 128 ones (Geo BN, Net::wide) for
+// molecules of 34 .. 64 atoms, whose primal + tangent P rows do not fit the LDS
+bool wide_tangent(const ecnf_cfg& c, int NT, int P) {
+  (void)P;
+  return NT && (c.mlp_width == 256 || (c.mlp_width == 128 && c.n_nodes > 33));
+}
 
 // Geo<NF, NT, P>::kSplitN: split node GEMMs, i.e. 16-B node-row strides (split primal kernels and, with
 // kSplitTanNode, the split tangent kernels)
@@ -426,6 +430,7 @@ void set_mpw(Net& n, const ecnf_cfg& c, int NT, int P, int mpw, int rp) {
   const int M = c.mlp_width, H = c.hidden, T = c.time_embedding_dim;
   n.MPW = mpw;
   n.RP = rp;
+  n.wide = wide_tangent(c, NT, P) && M == 128 ? 1 : 0;
   const bool vec = split_primal(c, NT, P);
   n.cross = vec && n.SR == c.n_nodes - 1 &&
             (size_t)mpw * (n.EP / 32) * ld_node(M, 1, true) <= (size_t)rp * ld_node(H + T, 1, true) &&
@@ -454,7 +459,8 @@ int choose_mpw(const ecnf_cfg& c, int NT, int P, int* mpw_out, size_t* lds_out, 
   for (int m = 1; m <= 32; ++m) {
     const int RP = 32 * ((m * N + 31) / 32);
     const bool vec = vec_layout(c, NT, P), wide = wide_tangent(c, NT, P);
-    if (wide && RP != 32) break;   // in-place phi_h: one 32-row node tile (node_gemm_inplace)
+    // in-place phi_h (node_gemm_inplace): one (output block pair, 32-row tile) task per wave of the 4-wave kernels
+    if (wide && (M / 64) * (RP / 32) > 4) break;
     const int floats = (NT ? lds_eval_floats<1>(N, D, H, T, M, c.mlp_depth, m, RP, vec, wide)
                            : lds_eval_floats<0>(N, D, H, T, M, c.mlp_depth, m, RP, vec)) +
                        solver_lds_floats(m, N * D);

@@ -119,7 +119,7 @@ __device__ inline bool check_features(const Net& net, int* f) {
 
 // one evaluation of the joint field g(tau, y) = dir * f(dir * tau, y) at (st.ts, st.ys) for every molecule
 // of the workgroup; writes kx_out [MPW][ND] and kl_out [MPW].  Exactly one egnn_eval call site (it is inlined).
-template <int NF, int NT, int L, int D, int P, bool TEAM, bool COLS>
+template <int NF, int NT, int L, int D, int P, bool TEAM, bool COLS, bool BN>
 __device__ __forceinline__ void joint_field(const Net& net, const Lds& s, const SolverLds& st, const SolveP& sp,
                                             float* kx_out, float* kl_out, const TeamCtx* tm, int* tepoch) {
   constexpr int kThreads = kernel_threads<NF, NT, P, COLS>();
@@ -154,7 +154,7 @@ __device__ __forceinline__ void joint_field(const Net& net, const Lds& s, const 
                     ? sp.pcache + (size_t)blockIdx.x * MPW * (net.N * (NF * 32) + 2 * net.N * D)
                     : nullptr;
     ECNF_DCHECK(!pc || (int)(blockIdx.x + 1) * MPW <= sp.pcache_slots, 6);
-    egnn_eval<NF, NT, L, D, P, TEAM, COLS>(net, s, st.ys, st.ts, st.tin, st.vout, st.tout, st.active, sparse ? k / D : -1,
+    egnn_eval<NF, NT, L, D, P, TEAM, COLS, BN>(net, s, st.ys, st.ts, st.tin, st.vout, st.tout, st.active, sparse ? k / D : -1,
                                      pc, k0 == 0 ? 1 : 2, tm, tepoch);
     tid = opaque_tid();
     if constexpr (NT) {
@@ -188,7 +188,7 @@ enum Phase { kEuler = 0, kInit0 = 1, kInit1 = 2, kFsal = 3, kStage = 4 };
 
 // The whole solve as a phase machine around ONE field evaluation per loop trip.  TEAM: the team (latency) mode
 // instantiation (egnn_eval.hpp team_exchange; launched only with sp.team.G > 1, compiled for team_shape)
-template <int NF, int NT, int L, int D, int P, bool TEAM = false, bool COLS = false>
+template <int NF, int NT, int L, int D, int P, bool TEAM = false, bool COLS = false, bool BN = false>
 __global__ __launch_bounds__((kernel_threads<NF, NT, P, COLS>())) __attribute__((amdgpu_waves_per_eu(Geo<NF, NT, P>::WPE))) void integrate_kernel(Net net, SolveP sp, const float* __restrict__ y0,
                                                                   const int32_t* __restrict__ feat,
                                                                   const float* __restrict__ eps, float* y1,
@@ -197,7 +197,7 @@ __global__ __launch_bounds__((kernel_threads<NF, NT, P, COLS>())) __attribute__(
   constexpr int kThreads = kernel_threads<NF, NT, P, COLS>();
   extern __shared__ float smem[];
   const int tid = (int)threadIdx.x, MPW = net.MPW, ND = net.ND, N = net.N;
-  const Lds s = carve_lds<NT, Geo<NF, NT, P>::kSplitN, Geo<NF, NT, P>::kNoP>(net, smem);
+  const Lds s = carve_lds<NT, Geo<NF, NT, P, BN>::kSplitN, Geo<NF, NT, P, BN>::kNoP>(net, smem);
   const SolverLds st = carve_solver(s.tail, MPW, ND);
   // team mode: workgroup blockIdx = T G + r is member r of molecule T's team (MPW = 1); only member 0 writes outputs
   TeamCtx team_ctx;
@@ -309,7 +309,7 @@ __global__ __launch_bounds__((kernel_threads<NF, NT, P, COLS>())) __attribute__(
     }
     __syncthreads();
 
-    joint_field<NF, NT, L, D, P, TEAM, COLS>(net, s, st, sp, kx_out, kl_out, tm, &tepoch);
+    joint_field<NF, NT, L, D, P, TEAM, COLS, BN>(net, s, st, sp, kx_out, kl_out, tm, &tepoch);
 
     // ------------------------------------------------ consume it
     {
@@ -492,7 +492,7 @@ __global__ __launch_bounds__((kernel_threads<NF, NT, P, COLS>())) __attribute__(
 }
 
 // one evaluation (and n_tangents JVPs) per molecule
-template <int NF, int NT, int L, int D, int P>
+template <int NF, int NT, int L, int D, int P, bool BN = false>
 __global__ __launch_bounds__((Geo<NF, NT, P>::NTHR)) __attribute__((amdgpu_waves_per_eu(Geo<NF, NT, P>::WPE))) void vf_kernel(Net net, const float* __restrict__ x,
                                                            const float* __restrict__ t,
                                                            const int32_t* __restrict__ feat,
@@ -501,7 +501,7 @@ __global__ __launch_bounds__((Geo<NF, NT, P>::NTHR)) __attribute__((amdgpu_waves
   constexpr int kThreads = Geo<NF, NT, P>::NTHR;
   extern __shared__ float smem[];
   const int tid = threadIdx.x, MPW = net.MPW, ND = net.ND, N = net.N;
-  const Lds s = carve_lds<NT, Geo<NF, NT, P>::kSplitN, Geo<NF, NT, P>::kNoP>(net, smem);
+  const Lds s = carve_lds<NT, Geo<NF, NT, P, BN>::kSplitN, Geo<NF, NT, P, BN>::kNoP>(net, smem);
   const SolverLds st = carve_solver(s.tail, MPW, ND);
   const int mol0 = blockIdx.x * MPW;
   const int nmol = min(MPW, B - mol0);
@@ -527,7 +527,7 @@ __global__ __launch_bounds__((Geo<NF, NT, P>::NTHR)) __attribute__((amdgpu_waves
         st.tin[i] = m < nmol ? tan_in[((size_t)(mol0 + m) * ntan + k) * ND + c] : 0.f;
       }
       __syncthreads();
-      egnn_eval<NF, 1, L, D, P>(net, s, st.ys, st.ts, st.tin, st.vout, st.tout);
+      egnn_eval<NF, 1, L, D, P, false, false, BN>(net, s, st.ys, st.ts, st.tin, st.vout, st.tout);
       for (int i = tid; i < nmol * ND; i += kThreads) {
         const int m = i / ND, c = i - m * ND;
         tan_out[((size_t)(mol0 + m) * ntan + k) * ND + c] = st.keep[m] ? kNaN : st.tout[i];
@@ -577,6 +577,10 @@ hipError_t launch_integrate(const Net& net, size_t lds, const SolveP& sp, const 
   }
   if (sp.team.G > 1) return hipErrorInvalidValue;   // no team kernel for this shape (team_size never asks for one)
   auto k = integrate_kernel<NF, NT, L, D, P>;
+  if constexpr (NT == 1 && NF == 4) {   // molecules of 34 .. 64 atoms: the wide (no P rows) form (Net::wide)
+    if (net.wide) k = integrate_kernel<NF, NT, L, D, P, false, false, true>;
+  }
+  if (net.wide && !(NT == 1 && NF == 4)) return hipErrorInvalidValue;
   hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
   const int grid = (B + net.MPW - 1) / net.MPW;
@@ -589,6 +593,10 @@ template <int NF, int NT, int L, int D, int P>
 hipError_t launch_vf(const Net& net, size_t lds, const float* x, const float* t, const int32_t* feat,
                      const float* tan_in, int ntan, float* v, float* tan_out, int B, hipStream_t stream) {
   auto k = vf_kernel<NF, NT, L, D, P>;
+  if constexpr (NT == 1 && NF == 4) {
+    if (net.wide) k = vf_kernel<NF, NT, L, D, P, true>;
+  }
+  if (net.wide && !(NT == 1 && NF == 4)) return hipErrorInvalidValue;
   hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
   const int grid = (B + net.MPW - 1) / net.MPW;

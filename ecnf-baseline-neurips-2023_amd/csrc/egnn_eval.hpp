@@ -52,22 +52,25 @@ constexpr bool kSplitTanNode = true;
 // P: GEMM arithmetic of the kernel.  P = 0 (ECNF_PREC_SPLIT_F16, the default) as described above; P = 1
 // (ECNF_PREC_FP32, ecnf_set_precision) every GEMM on v_mfma_f32_32x32x2_f32 with fp32 operands: the strict-fp32
 // comparator and the fallback for molecules whose activations leave the fp16 range (ECNF_E_NONFINITE).
-template <int NF, int NT, int P = 0>
+// BN ("big N"): the M = 128 tangent kernels in the wide form (kWideT / kWideT32: per-edge phi_e.0, no P rows) for
+// molecules of 34 .. 64 atoms, whose P rows (primal + tangent) do not fit the LDS beside the rest.
+template <int NF, int NT, int P = 0, bool BN = false>
 struct Geo {
+  static_assert(!BN || (NT == 1 && NF == 4), "the big-N form is an M = 128 tangent kernel");
   static constexpr bool kSplit = kSplitChain && P == 0 && NT == 0 && NF <= kSplitMaxNF;
   // tangent kernels: the edge chains run split (chain_split_tangent); node GEMMs, layer 1 and the tail stay fp32
-  static constexpr bool kSplitT = kSplitTanChain && P == 0 && NT == 1 && NF <= 4;
+  static constexpr bool kSplitT = kSplitTanChain && P == 0 && NT == 1 && NF <= 4 && !BN;
   // node GEMMs on the split path with 16-B node-row strides: the split primal kernels and (kSplitTanNode) the
   // M <= 128 tangent kernels (log2-domain P via the primal Wp_s; tangent rows share every A fragment).  (The padded
   // 16-B strides fit ALDP's M = 64 tangent kernel at 2 molecules per workgroup only since the x_c0 copy left LDS
   // and vecs is sized by L: before, split node GEMMs dropped it to 1, 55.9 -> 62.0 ms.)
-  // M = 256 tangent kernels (QM9): per-edge phi_e.0 (no P buffer), sequential primal / tangent split chains
-  // (chain_dual_seq), phi_h in place on macc
-  static constexpr bool kWideT = kSplitTanChain && P == 0 && NT == 1 && NF == 8;
+  // M = 256 tangent kernels (QM9), and the big-N M = 128 ones: per-edge phi_e.0 (no P buffer), sequential primal /
+  // tangent split chains (chain_dual_seq), phi_h in place on macc
+  static constexpr bool kWideT = kSplitTanChain && P == 0 && NT == 1 && (NF == 8 || BN);
   // M = 256 strict-fp32 tangent kernels (P = 1): kWideT's structure on v_mfma_f32_32x32x2_f32 (per-edge phi_e.0
   // from the fp32 kernel rows, sequential primal / tangent chain passes, in-place phi_h): the fallback for QM9
   // divergence solves whose activations leave the fp16 range and for checkpoints with edge weights >= 2^15
-  static constexpr bool kWideT32 = P == 1 && NT == 1 && NF == 8;
+  static constexpr bool kWideT32 = P == 1 && NT == 1 && (NF == 8 || BN);
   static constexpr bool kNoP = kWideT || kWideT32;   // no per-node phi_e.0 halves (P rows) in LDS
   static constexpr bool kSplitN = kSplit || (kSplitTanNode && kSplitT) || kWideT;
   // M <= 128 split tangent kernels: P (primal and tangent rows) in the log2 domain (the primal kernels' -log2(e)
@@ -169,6 +172,7 @@ struct Net {
   float nn1;      // avg_num_neighbours = N - 1
   float sqrt_nn1; // sqrt(N - 1) in fp32
   int cross;      // split kernels: message segment parts are stored, not atomically added (Lds::cross)
+  int wide;       // M = 128 tangent kernels in the wide form (Geo BN: per-edge phi_e.0, no P rows; 34 .. 64 atoms)
   int ncross;     // receiver segments per molecule that cross a tile boundary (split kernels with cross)
   unsigned char xs_i[kMaxTilesPerMol];   // ... their receiver atom i
   unsigned char xs_t[kMaxTilesPerMol];   // ... and the molecule tile that holds their continuation part
@@ -668,17 +672,19 @@ __device__ __forceinline__ void node_gemm(const float* X1, int ldx1, int K1, con
                      task / njb, lane);
 }
 
-// in-place split node GEMM (Y aliases X1; the M = 256 tangent kernels' phi_h on macc): output block pairs, at most one
-// task per wave (the host admits these kernels only for RP = 32 rows: (NOUT / 64) tasks <= NW)
+// in-place split node GEMM (Y aliases X1; the wide tangent kernels' phi_h on macc): one (output block pair, 32-row
+// tile) task per wave at most (the host admits these kernels only where (NOUT / 64) (RP / 32) <= NW: M = 256 at one
+// row tile, M = 128 at two)
 template <int NT, int NW>
 __device__ __forceinline__ void node_gemm_inplace(const float* X1, int ldx1, int K1, const float* X2, int ldx2, int K2,
                                                   const unsigned* __restrict__ Ws, float winv,
                                                   const float* __restrict__ bias, int NOUT, bool act, float* Y, int ldy,
                                                   int RP, int nvalid, int wave, int lane) {
-  const int npair = NOUT >> 6;
-  const bool active = wave < npair;
+  const int npair = NOUT >> 6, ntask = npair * (RP >> 5);
+  const bool active = wave < ntask;
+  ECNF_DCHECK(ntask <= NW, 3);
   node_task_split<2, NT, true>(X1, ldx1, K1, X2, ldx2, K2, Ws, winv, bias, act, nullptr, 0, Y, ldy, RP, nvalid,
-                               active ? 2 * wave : 0, 0, lane, active);
+                               active ? 2 * (wave % npair) : 0, active ? wave / npair : 0, lane, active);
 }
 
 // the same in strict fp32 (the M = 256 fp32 tangent kernels, Geo::kWideT32): node_task's k-loop and epilogue on
@@ -688,11 +694,11 @@ __device__ __forceinline__ void node_gemm_inplace_f32(const float* X1, int ldx1,
                                                       int K2, const float* __restrict__ W, int ldw,
                                                       const float* __restrict__ bias, int NOUT, bool act, float* Y,
                                                       int ldy, int RP, int nvalid, int wave, int lane) {
-  const int npair = NOUT >> 6;
-  const bool active = wave < npair;
-  const int jb = active ? 2 * wave : 0;
-  const int kk = lane >> 5, li = lane & 31;
-  ECNF_DCHECK(!active || RP == 32, 3);
+  const int npair = NOUT >> 6, ntask = npair * (RP >> 5);
+  const bool active = wave < ntask;
+  const int jb = active ? 2 * (wave % npair) : 0, ct = active ? wave / npair : 0;
+  const int kk = lane >> 5, li = lane & 31, n = ct * 32 + li;
+  ECNF_DCHECK(ntask <= NW, 3);
   f32x16 acc[2], accT[2];
 #pragma unroll
   for (int a = 0; a < 2; ++a) {
@@ -702,12 +708,12 @@ __device__ __forceinline__ void node_gemm_inplace_f32(const float* X1, int ldx1,
   }
   if (active) {
     const gfloat_p wcol = gptr(W) + kk * ldw + jb * 32 + li;
-    node_kloop<NT, 2>(acc, accT, wcol, ldw, X1 + li * ldx1 + kk, X1 + (RP + li) * ldx1 + kk, K1);
+    node_kloop<NT, 2>(acc, accT, wcol, ldw, X1 + n * ldx1 + kk, X1 + (RP + n) * ldx1 + kk, K1);
     if (K2 > 0)
-      node_kloop<NT, 2>(acc, accT, wcol + K1 * ldw, ldw, X2 + li * ldx2 + kk, X2 + (RP + li) * ldx2 + kk, K2);
+      node_kloop<NT, 2>(acc, accT, wcol + K1 * ldw, ldw, X2 + n * ldx2 + kk, X2 + (RP + n) * ldx2 + kk, K2);
   }
   __syncthreads();
-  if (active) node_epilogue<NT, 2>(acc, accT, act, nullptr, 0, Y, ldy, RP, nvalid, jb, li, kk);
+  if (active) node_epilogue<NT, 2>(acc, accT, act, nullptr, 0, Y, ldy, RP, nvalid, jb, n, kk);
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -1208,7 +1214,7 @@ __device__ __forceinline__ void chain_dual_seq_f32(f32x16 (&X)[NF], f32x16 (&XT)
 //   amode 2 (last block): the edges INTO atoms 0 and a (receiver 0's N - 1 edges, then receiver a's; a >= 1)
 // WPP: weight pieces of the primal split chain (kSplit branch): 2 in the primal kernels, 3 (exact weights, as the
 // dual tiles' primal) for the exact trace's primal-only tiles inside the divergence kernels
-template <int NF, int NT, int L, int D, int P, int WPP = kPieces>
+template <int NF, int NT, int L, int D, int P, int WPP = kPieces, bool BN = false>
 __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, const Lds& s, int tile, int lane, bool agg,
                                           int a = -1, int part = 0, int amode = 1) {
   const int kk = lane >> 5, li = lane & 31;
@@ -1226,7 +1232,7 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
     sd = i + 1 + (valid ? j0 : 0);
     if (sd >= N) sd -= N;
   } else {
-    ECNF_DCHECK((Geo<NF, NT, P>::kL2T && tile < net.MPW && a < N), 6);
+    ECNF_DCHECK((Geo<NF, NT, P, BN>::kL2T && tile < net.MPW && a < N), 6);
     mol = tile;
     const int q = part * 32 + li;
     valid = q < 2 * nn1;
@@ -1256,7 +1262,7 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
   // split kernels: the row this lane's receiver-segment part is stored to — macc for the part in the tile where
   // the segment starts, the cross buffer (one row per molecule tile) for its continuation in the next tile
   float* agg_dst = nullptr;
-  if constexpr (Geo<NF, NT, P>::kSplit) {
+  if constexpr (Geo<NF, NT, P, BN>::kSplit) {
     if (net.cross) {
       const int tloc = tile - mrow * (net.EP >> 5);
       agg_dst = tloc == ((i * nn1) >> 5) ? s.macc + rr * s.ld_m : s.cross + (mrow * (net.EP >> 5) + tloc) * s.ld_m;
@@ -1293,7 +1299,7 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
     for (int d = 0; d < D; ++d) dr[d] = 0.f;
   }
 
-  if constexpr (Geo<NF, NT, P>::kSplit) {
+  if constexpr (Geo<NF, NT, P, BN>::kSplit) {
     // phi_e layer 1 from the per-node halves: pre = P_s[s] + P_r[r] + |r|^2 w_d  (egnn.py:76,79), SiLU, split
     SplitX<NF> XA, XB;
     f32x16 acc[NF];
@@ -1347,7 +1353,7 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
     STAMP_LANE0(s, kStEdgeTail, t_sub);
     return;
   }
-  if constexpr (Geo<NF, NT, P>::kL2T) {
+  if constexpr (Geo<NF, NT, P, BN>::kL2T) {
     // phi_e.0 from the log2-domain per-node halves: u = P_s[s] + P_r[r] + |r|^2 w_d', y' = u / (1 + 2^u) and its
     // tangent dy' = r du (1 - ln2 (u - y')), split straight into the chain's input buffers (16-B LDS reads)
     constexpr float kNegLn2 = -0.69314718055994531f;
@@ -1416,7 +1422,7 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
     STAMP_LANE0(s, kStEdgeTail, t_sub);
     return;
   }
-  if constexpr (Geo<NF, NT, P>::kWideT) {
+  if constexpr (Geo<NF, NT, P, BN>::kWideT) {
     // M = 256 tangent kernels: phi_e.0 per edge, then the sequential dual chains (chain_dual_seq)
     f32x16 X[NF], XT[NF];
     edge_layer1_dual<NF>(net, bw, s, rr, rs, len2, dlen2, X, XT, lane);
@@ -1433,7 +1439,7 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
     STAMP_LANE0(s, kStEdgeTail, t_sub);
     return;
   }
-  if constexpr (Geo<NF, NT, P>::kWideT32) {
+  if constexpr (Geo<NF, NT, P, BN>::kWideT32) {
     // the same in strict fp32 (natural-domain activations and biases, the fp32 chain fragments)
     f32x16 X[NF], XT[NF];
     edge_layer1_dual_f32<NF>(net, bw, s, rr, rs, len2, dlen2, X, XT, lane);
@@ -1477,7 +1483,7 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
   STAMP_LANE0(s, kStEdgeLayer1, t_sub);
   // phi_e layers 2..L.  The weight pointer is laundered through an empty asm so the (tile-invariant) weight
   // loads are not hoisted out of the tile loop into thousands of live registers.
-  if constexpr (Geo<NF, NT, P>::kSplitT) {
+  if constexpr (Geo<NF, NT, P, BN>::kSplitT) {
     // split-fp16 chains with tangents (chain_split_tangent; the staged chain biases are the log2-domain copies)
     ChainInv ie, ix;
     static_for<2 * 4 - 1>([&](auto Lc) {
@@ -1946,19 +1952,19 @@ __device__ __forceinline__ void team_exchange(const Net& net, const Lds& s, cons
 // one full evaluation.  x_in/tan_in/v_out/tan_out: LDS [MPW][N*D]; t_in: LDS [MPW] (actual time).
 // Must be called by all Geo<NF, NT, P>::NTHR threads of the workgroup (NW waves); returns after a barrier.
 // ---------------------------------------------------------------------------------------------------
-template <int NF, int NT, int L, int D, int P, bool TEAM = false, bool COLS = false>
+template <int NF, int NT, int L, int D, int P, bool TEAM = false, bool COLS = false, bool BN = false>
 __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const float* x_in, const float* t_in, const float* tan_in,
                           float* v_out, float* tan_out, const int* act = nullptr, int sparse_a = -1,
                           float* pcache = nullptr, int pmode = 0, const TeamCtx* tm = nullptr,
                           int* tepoch = nullptr) {
   constexpr int kNW = kernel_waves<NF, NT, P, COLS>(), kNT = kernel_threads<NF, NT, P, COLS>();
-  constexpr bool kSplitG = Geo<NF, NT, P>::kSplit;
-  constexpr bool kSplitN = Geo<NF, NT, P>::kSplitN;   // split node GEMMs (primal split kernels and tangent kernels)
+  constexpr bool kSplitG = Geo<NF, NT, P, BN>::kSplit;
+  constexpr bool kSplitN = Geo<NF, NT, P, BN>::kSplitN;   // split node GEMMs (primal split kernels and tangent kernels)
   // the exact trace's sparse blocks (primal + dual tiles, see the edge loop) in the M <= 128 split tangent kernels;
   // not compiled for the L = 2 shapes (M, D) = (128, 3), (64, 2), where the primal tile's code beside the dual
   // tile's spilled 36 B per lane (tests/test_kernel_resources.py).  The BASELINE shapes (LJ13 128/3/3, ALDP 64/2/3,
   // DW4 128/3/2) have it.
-  constexpr bool kSparseX = Geo<NF, NT, P>::kL2T && !(L == 2 && (NF == 4 || D == 2));
+  constexpr bool kSparseX = Geo<NF, NT, P, BN>::kL2T && !(L == 2 && (NF == 4 || D == 2));
   const int tid = opaque_tid(), lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: task indices stay in SGPRs
   const int N = net.N, H = net.H, T = net.T, M = NF * 32, RP = net.RP, MPW = net.MPW, ND = net.ND;
@@ -2012,10 +2018,10 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
     const bool need_h = k + 1 < net.K;
     // stage this block's chain biases and the w_d / w_g / w_x vectors in LDS (read by every edge tile)
     {
-      const float* be = (kSplitG || Geo<NF, NT, P>::kSplitT || Geo<NF, NT, P>::kWideT) ? bw.be_u : bw.be;
-      const float* wd = (kSplitG || Geo<NF, NT, P>::kL2T) ? bw.wd_u : bw.wd;
-      const float* wg = (kSplitG || Geo<NF, NT, P>::kL2T) ? bw.wg_u : bw.wg;
-      const float* wx = (kSplitG || Geo<NF, NT, P>::kL2T) ? bw.wx_u : bw.wx;
+      const float* be = (kSplitG || Geo<NF, NT, P, BN>::kSplitT || Geo<NF, NT, P, BN>::kWideT) ? bw.be_u : bw.be;
+      const float* wd = (kSplitG || Geo<NF, NT, P, BN>::kL2T) ? bw.wd_u : bw.wd;
+      const float* wg = (kSplitG || Geo<NF, NT, P, BN>::kL2T) ? bw.wg_u : bw.wg;
+      const float* wx = (kSplitG || Geo<NF, NT, P, BN>::kL2T) ? bw.wx_u : bw.wx;
       for (int idx = tid; idx < (2 * L + 2) * M; idx += kNT) {
         const int v = idx / M, c = idx - v * M;
         float val;
@@ -2027,14 +2033,14 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
       }
     }
     // h <- Dense([h | temb])  (egnn.py:166-167)
-    node_gemm<NT, kNW, kSplitN, Geo<NF, NT, P>::kNodePFA>(s.hin, s.ld_hin, H + T, nullptr, 0, 0, bw.Wn, bw.Wn_s, bw.ninv, H, bw.bn, H,
+    node_gemm<NT, kNW, kSplitN, Geo<NF, NT, P, BN>::kNodePFA>(s.hin, s.ld_hin, H + T, nullptr, 0, 0, bw.Wn, bw.Wn_s, bw.ninv, H, bw.bn, H,
                                       false, nullptr, 0, s.hb, s.ld_hb, RP, nvalid, wave, lane);
     __syncthreads();
     STAMP(s, kStNodeDense);
     // per-node halves of phi_e layer 1 (the M = 256 tangent kernels compute layer 1 per edge)
-    if constexpr (!Geo<NF, NT, P>::kNoP) {
-      constexpr bool kPu = kSplitG || Geo<NF, NT, P>::kL2T;   // log2-domain P
-      node_gemm<NT, kNW, kSplitN, Geo<NF, NT, P>::kNodePFA>(s.hb, s.ld_hb, H, nullptr, 0, 0, bw.Wp, bw.Wp_s, bw.pinv, 2 * M,
+    if constexpr (!Geo<NF, NT, P, BN>::kNoP) {
+      constexpr bool kPu = kSplitG || Geo<NF, NT, P, BN>::kL2T;   // log2-domain P
+      node_gemm<NT, kNW, kSplitN, Geo<NF, NT, P, BN>::kNodePFA>(s.hb, s.ld_hb, H, nullptr, 0, 0, bw.Wp, bw.Wp_s, bw.pinv, 2 * M,
                                         kPu ? bw.bp_u : bw.bp, 2 * M, false, nullptr, 0, s.P, s.ld_P, RP, nvalid, wave,
                                         lane);
       __syncthreads();
@@ -2096,7 +2102,7 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
       const int tstep = TEAM ? tm->p.G : 1, tfirst = TEAM ? tm->r : 0;
       if constexpr (COLS) {
         // column-split team mode: member r runs tile r (G = tiles per molecule) with all of its waves
-        static_assert(TEAM && NT == 0 && Geo<NF, NT, P>::kSplit, "cols mode: team primal split kernels");
+        static_assert(TEAM && NT == 0 && Geo<NF, NT, P, BN>::kSplit, "cols mode: team primal split kernels");
         for (int vt = tfirst; vt < nrun; vt += tstep) {
           const int q = vt / tpm;
           edge_tile_cols<NF, L, D>(net, bw, s, nth_active(q) * tpm + (vt - q * tpm), wave, elane, need_h);
@@ -2106,7 +2112,7 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
         if constexpr (kSparseX) {
           if (vt < nd) {
             const int q = vt / ndt;
-            edge_tile<NF, NT, L, D, P>(net, bw, s, nth_active(q), elane, need_h, sparse_a, vt - q * ndt, amode);
+            edge_tile<NF, NT, L, D, P, kPieces, BN>(net, bw, s, nth_active(q), elane, need_h, sparse_a, vt - q * ndt, amode);
             continue;
           }
         }
@@ -2118,7 +2124,7 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
             continue;
           }
         }
-        edge_tile<NF, NT, L, D, P>(net, bw, s, tile, elane, need_h);
+        edge_tile<NF, NT, L, D, P, kPieces, BN>(net, bw, s, tile, elane, need_h);
       }
       }   // !COLS
     }
@@ -2171,7 +2177,7 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
           for (int c = lane; c < M; c += 64) dst[c] += src[c];
         }
       }
-    } else if constexpr (!Geo<NF, NT, P>::kL2T) {   // kL2T: the scale is in the split phi_h.0 weights
+    } else if constexpr (!Geo<NF, NT, P, BN>::kL2T) {   // kL2T: the scale is in the split phi_h.0 weights
       for (int idx = tid; idx < R * M; idx += kNT) {
         const int row = idx / M, c = idx - row * M;
         s.macc[row * s.ld_m + c] = s.macc[row * s.ld_m + c] / net.sqrt_nn1;
@@ -2188,7 +2194,7 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
     }
     STAMP(s, kStNodeUpd);
     // phi_h = MLP((M,)*L + (H,)) on [m_i | h], residual (egnn.py:105-111)
-    if constexpr (Geo<NF, NT, P>::kWideT) {
+    if constexpr (Geo<NF, NT, P, BN>::kWideT) {
       // in place on macc (no P region in these kernels), then macc restarts from +0 for the next block's aggregates
       node_gemm_inplace<NT, kNW>(s.macc, s.ld_m, M, s.hb, s.ld_hb, H, bw.Wh_sn0, bw.hinv_n0, bw.bh[0], M, true,
                                  s.macc, s.ld_m, RP, nvalid, wave, lane);
@@ -2209,7 +2215,7 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
       STAMP(s, kStPhiH);
       continue;
     }
-    if constexpr (Geo<NF, NT, P>::kWideT32) {   // the same in fp32 (macc already carries the 1 / sqrt(N - 1))
+    if constexpr (Geo<NF, NT, P, BN>::kWideT32) {   // the same in fp32 (macc already carries the 1 / sqrt(N - 1))
       node_gemm_inplace_f32<NT, kNW>(s.macc, s.ld_m, M, s.hb, s.ld_hb, H, bw.Wh[0], M, bw.bh[0], M, true, s.macc,
                                      s.ld_m, RP, nvalid, wave, lane);
       __syncthreads();
@@ -2231,8 +2237,8 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
     }
     float* Q0 = s.P;
     float* Q1 = s.P + (kSplitN ? M + 4 : M + 1);   // 16-B aligned rows for the split node GEMMs
-    constexpr bool kHu = kSplitG || Geo<NF, NT, P>::kL2T;   // log2-domain messages, scale in phi_h.0
-    node_gemm<NT, kNW, kSplitN, Geo<NF, NT, P>::kNodePFA>(s.macc, s.ld_m, M, s.hb, s.ld_hb, H, bw.Wh[0], kHu ? bw.Wh_s[0] : bw.Wh_sn0,
+    constexpr bool kHu = kSplitG || Geo<NF, NT, P, BN>::kL2T;   // log2-domain messages, scale in phi_h.0
+    node_gemm<NT, kNW, kSplitN, Geo<NF, NT, P, BN>::kNodePFA>(s.macc, s.ld_m, M, s.hb, s.ld_hb, H, bw.Wh[0], kHu ? bw.Wh_s[0] : bw.Wh_sn0,
                                       kHu ? bw.hinv[0] : bw.hinv_n0, M, bw.bh[0], M, true, nullptr, 0, Q0, s.ld_P, RP,
                                       nvalid, wave, lane);
     __syncthreads();
@@ -2243,12 +2249,12 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
       }
     }
     for (int l = 1; l < L; ++l) {
-      node_gemm<NT, kNW, kSplitN, Geo<NF, NT, P>::kNodePFA>(Q0, s.ld_P, M, nullptr, 0, 0, bw.Wh[l], bw.Wh_s[l], bw.hinv[l], M, bw.bh[l], M,
+      node_gemm<NT, kNW, kSplitN, Geo<NF, NT, P, BN>::kNodePFA>(Q0, s.ld_P, M, nullptr, 0, 0, bw.Wh[l], bw.Wh_s[l], bw.hinv[l], M, bw.bh[l], M,
                                         true, nullptr, 0, Q1, s.ld_P, RP, nvalid, wave, lane);
       __syncthreads();
       float* tq = Q0; Q0 = Q1; Q1 = tq;
     }
-    node_gemm<NT, kNW, kSplitN, Geo<NF, NT, P>::kNodePFA>(Q0, s.ld_P, M, nullptr, 0, 0, bw.Wh[L], bw.Wh_s[L], bw.hinv[L], H, bw.bh[L], H,
+    node_gemm<NT, kNW, kSplitN, Geo<NF, NT, P, BN>::kNodePFA>(Q0, s.ld_P, M, nullptr, 0, 0, bw.Wh[L], bw.Wh_s[L], bw.hinv[L], H, bw.bh[L], H,
                                       false, s.hb, s.ld_hb, s.hin, s.ld_hin, RP, nvalid, wave, lane);
     __syncthreads();
     STAMP(s, kStPhiH);

@@ -82,3 +82,21 @@ def test_aggregation_atomics_are_flat(disassembly):
         flat_kernels += sum(1 for f in best)
     assert flat_kernels > 0
     assert not bad, "\n".join(bad[:10])
+
+
+def test_integrate_kernels_never_touch_scratch(disassembly):
+    """No spill or private-memory access in any split-precision (P = 0) integrate kernel's ISA (the solve loop keeps
+    everything in registers and LDS; test_kernel_resources.py reads the reserved private-segment sizes, which can be
+    non-zero and unreferenced).  The strict-fp32 comparator kernels (P = 1) keep their bounded spills."""
+    bad = {}
+    for p in disassembly:
+        fn = None
+        for line in open(p):
+            m = re.match(r"^[0-9a-f]+ <(.*)>:", line)
+            if m:
+                fn = m.group(1)
+                continue
+            split = fn and re.search(r"integrate_kernelILi\d+ELi\d+ELi\d+ELi\d+ELi0E", fn)
+            if split and re.search(r"\bscratch_(load|store)", line):
+                bad[fn] = bad.get(fn, 0) + 1
+    assert not bad, bad

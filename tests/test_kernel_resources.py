@@ -17,8 +17,10 @@ pytestmark = pytest.mark.skipif(not (os.path.exists(KR.LIB) and os.path.exists(f
                                      and shutil.which("c++filt")),
                                 reason="needs the built library and the ROCm LLVM tools")
 
-# template arguments <NF, NT, L, D, P> of integrate_kernel / vf_kernel
-SIG = re.compile(r"(integrate_kernel|vf_kernel)<(\d+), (\d+), (\d+), (\d+), (\d+)>")
+# template arguments <NF, NT, L, D, P, ...> of integrate_kernel (TEAM, COLS, BN follow) / vf_kernel (BN follows).
+# (Up to round 4 this pattern ended at the fifth argument with '>', which the integrate kernels' extra flags never
+# matched: their scratch limits were not checked.)
+SIG = re.compile(r"(integrate_kernel|vf_kernel)<(\d+), (\d+), (\d+), (\d+), (\d+)[,>]")
 
 
 def _kernels():
@@ -34,7 +36,8 @@ def _kernels():
 
 def test_split_kernels_do_not_spill():
     ks = _kernels()
-    assert len(ks) >= 40, "expected the integrate / vf kernels of every compiled shape"
+    assert len(ks) >= 80, "expected the integrate / vf kernels of every compiled shape"
+    assert sum(k[0] == "integrate_kernel" for k in ks) >= 40
     bad = []
     for kind, nf, nt, l, d, p, scratch in ks:
         if p != 0:
@@ -46,8 +49,10 @@ def test_split_kernels_do_not_spill():
         # tangent form keeps 28 B per lane outside its edge tiles (2 waves per SIMD at 256 registers); the split
         # primal forms report a 20 B private segment that no instruction of theirs addresses (no scratch_* in their
         # ISA, round 4)
-        limit = (0 if kind == "integrate_kernel" else 28 if (nf == 2 and nt == 1) else 96 if (nf == 8 and nt == 1)
-                 else 20 if nt == 0 else 0)
+        # The M = 256 tangent integrate kernels report a 20 B private segment that, like the split primal vf_kernel's,
+        # no instruction addresses (tests/test_isa_hazards.py: no scratch instruction in any integrate kernel).
+        limit = ((20 if (nf == 8 and nt == 1) else 0) if kind == "integrate_kernel" else 28 if (nf == 2 and nt == 1)
+                 else 96 if (nf == 8 and nt == 1) else 20 if nt == 0 else 0)
         if scratch > limit:
             bad.append(f"{kind}<{nf},{nt},{l},{d},{p}> scratch {scratch} B/lane (limit {limit})")
     assert not bad, "\n".join(bad)
