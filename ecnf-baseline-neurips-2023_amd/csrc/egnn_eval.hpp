@@ -879,6 +879,38 @@ __device__ __forceinline__ void lds_add(float* p, float v) {
   __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+// d = w . x (and dT = w . xT) over the lane's NF x 16 feature registers, w an LDS vector in accumulator row order
+// (rows acc_row(r, kk), 16-B reads); the caller adds the other lane half.  Four partial sums, and the weight reads
+// issued one group of 4 ahead behind scheduling fences: the one-accumulator form compiled to 4 NF rounds of
+// read -> s_waitcnt lgkmcnt(0) -> 4 dependent FMAs, exposing the LDS latency and the FMA chain 4 NF times per tile.
+template <int NF, int NT>
+__device__ __forceinline__ void lds_dot(const float* __restrict__ w, const f32x16 (&x)[NF], const f32x16 (&xt)[NF],
+                                        int kk, float& d, float& dT) {
+  // (2 reads per group in the M = 256 tangent kernels, whose 512-register waves have no 32 registers to spare)
+  constexpr int NQ = 4 * NF, GQ = (NT && NF >= 8) ? 2 : 4, NG = NQ / GQ;
+  auto rd = [&](int q) { return *reinterpret_cast<const f32x4*>(w + (q >> 2) * 32 + 8 * (q & 3) + 4 * kk); };
+  f32x4 wb[2][GQ];
+  float p[4] = {0.f, 0.f, 0.f, 0.f}, pt[4] = {0.f, 0.f, 0.f, 0.f};
+  static_for<GQ>([&](auto Ic) { wb[0][decltype(Ic)::value] = rd(decltype(Ic)::value); });
+  static_for<NG>([&](auto Gc) {
+    constexpr int g = decltype(Gc)::value;
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (g + 1 < NG)
+      static_for<GQ>([&](auto Ic) { wb[(g + 1) & 1][decltype(Ic)::value] = rd((g + 1) * GQ + decltype(Ic)::value); });
+    static_for<GQ>([&](auto Ic) {
+      constexpr int q = g * GQ + decltype(Ic)::value, fb = q >> 2, qq = q & 3;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        p[e] = fmaf(wb[g & 1][decltype(Ic)::value][e], x[fb][4 * qq + e], p[e]);
+        if constexpr (NT) pt[e] = fmaf(wb[g & 1][decltype(Ic)::value][e], xt[fb][4 * qq + e], pt[e]);
+      }
+    });
+  });
+  __builtin_amdgcn_sched_barrier(0);
+  d = (p[0] + p[1]) + (p[2] + p[3]);
+  dT = NT ? (pt[0] + pt[1]) + (pt[2] + pt[3]) : 0.f;
+}
+
 // phi_x output Dense(1) (egnn.py:83-85), shifts_ij = phi_x * r_ij / (C + |r_ij|) and their segment sum
 // (egnn.py:87-94)
 template <int NF, int NT, int L, int D>
@@ -887,21 +919,14 @@ __device__ __forceinline__ void edge_shift(const Net& net, const BlockW& bw, con
                                            const float (&r)[D], const float (&dr)[D], float length, float dlength,
                                            int lane, bool pw = true) {
   const int kk = lane >> 5;
-  float phx = 0.f, phxT = 0.f;
-#pragma unroll
-  for (int fb = 0; fb < NF; ++fb)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const f32x4 w = *reinterpret_cast<const f32x4*>(s.vecs + (2 * L + 1) * (NF * 32) + fb * 32 + 8 * q + 4 * kk);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        phx += w[e] * px[fb][4 * q + e];
-        if constexpr (NT) phxT += w[e] * pxT[fb][4 * q + e];
-      }
-    }
+  float phx, phxT;
+  lds_dot<NF, NT>(s.vecs + (2 * L + 1) * (NF * 32), px, pxT, kk, phx, phxT);
   phx += __shfl_xor(phx, 32);
   if constexpr (NT) phxT += __shfl_xor(phxT, 32);
   phx += bw.bx;
+  // full-precision divisions, as the oracle: a reciprocal-multiply form (1 division instead of 2D) moved the DW4
+  // exact-trace PID solves outside their fp32-oracle envelope (tests/test_gpu_eval_modes.py; profiles/round5/dw4_envelope) and
+  // saved no measurable time
   const float den = net.C + length;
   const int RP = net.RP;
   float sh[2 * D];
@@ -939,18 +964,8 @@ __device__ __forceinline__ void edge_tail(const Net& net, const BlockW& bw, cons
   // on x alone, egnn.py:176-188): agg == false skips them (wave-uniform)
   if (agg) {
   // gate e_ij = sigmoid(m_ij . w_g + b_g)  (egnn.py:99-101)
-  float part = 0.f, partT = 0.f;
-#pragma unroll
-  for (int fb = 0; fb < NF; ++fb)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const f32x4 w = *reinterpret_cast<const f32x4*>(s.vecs + (2 * L) * (NF * 32) + fb * 32 + 8 * q + 4 * kk);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        part += w[e] * m[fb][4 * q + e];
-        if constexpr (NT) partT += w[e] * mT[fb][4 * q + e];
-      }
-    }
+  float part, partT;
+  lds_dot<NF, NT>(s.vecs + (2 * L) * (NF * 32), m, mT, kk, part, partT);
   part += __shfl_xor(part, 32);
   if constexpr (NT) partT += __shfl_xor(partT, 32);
   const float g = sigmoidf_(part + bw.bg);
@@ -1305,22 +1320,35 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
     f32x16 acc[NF];
     const float* Ps = s.P + rs * s.ld_P;
     const float* Pr = s.P + rr * s.ld_P + M;
-    static_for<NF>([&](auto Fc) {
-      constexpr int fb = decltype(Fc)::value;
-      static_for<4>([&](auto Qc) {
-        constexpr int q = decltype(Qc)::value;
-        const int row = fb * 32 + 8 * q + 4 * kk;   // 4 consecutive features: 16-B LDS reads
-        const f32x4 w = *reinterpret_cast<const f32x4*>(s.vecs + (2 * L - 1) * (NF * 32) + row);
-        const f32x4 ps = *reinterpret_cast<const f32x4*>(Ps + row);
-        const f32x4 pr = *reinterpret_cast<const f32x4*>(Pr + row);
+    // 4 NF rounds of 4 consecutive features (16-B LDS reads of w_d, P_s, P_r), two rounds per step behind
+    // scheduling fences with the next step's reads issued first: the per-round read -> s_waitcnt lgkmcnt(0) ->
+    // 2-element SiLU chain form exposed the LDS latency and a wait state after every transcendental
+    constexpr int NQ = 4 * NF, GQ = 2, NG = NQ / GQ;
+    auto rd3 = [&](int q, f32x4 (&o)[3]) {
+      const int row = (q >> 2) * 32 + 8 * (q & 3) + 4 * kk;
+      o[0] = *reinterpret_cast<const f32x4*>(s.vecs + (2 * L - 1) * (NF * 32) + row);
+      o[1] = *reinterpret_cast<const f32x4*>(Ps + row);
+      o[2] = *reinterpret_cast<const f32x4*>(Pr + row);
+    };
+    f32x4 lb[2][GQ][3];
+    static_for<GQ>([&](auto Ic) { rd3(decltype(Ic)::value, lb[0][decltype(Ic)::value]); });
+    static_for<NG>([&](auto Gc) {
+      constexpr int g = decltype(Gc)::value;
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (g + 1 < NG)
+        static_for<GQ>([&](auto Ic) { rd3((g + 1) * GQ + decltype(Ic)::value, lb[(g + 1) & 1][decltype(Ic)::value]); });
+      static_for<GQ>([&](auto Ic) {
+        constexpr int q = g * GQ + decltype(Ic)::value, fb = q >> 2, qq = q & 3;
+        const f32x4(&o)[3] = lb[g & 1][decltype(Ic)::value];
         static_for<2>([&](auto Hc) {
           constexpr int e = 2 * decltype(Hc)::value;
-          const float u0 = ps[e] + pr[e] + len2 * w[e];   // log2 domain (silu_u)
-          const float u1 = ps[e + 1] + pr[e + 1] + len2 * w[e + 1];
-          put_pair<NF, fb, 4 * q + e>(XA, silu_u(u0), silu_u(u1));
+          const float u0 = o[1][e] + o[2][e] + len2 * o[0][e];   // log2 domain (silu_u)
+          const float u1 = o[1][e + 1] + o[2][e + 1] + len2 * o[0][e + 1];
+          put_pair<NF, fb, 4 * qq + e>(XA, silu_u(u0), silu_u(u1));
         });
       });
     });
+    __builtin_amdgcn_sched_barrier(0);
     STAMP_LANE0(s, kStEdgeLayer1, t_sub);
     // phi_e layers 2..L
     const unsigned* Ws = launder_uniform(WPP == 3 ? bw.Ws3 : bw.Ws);
@@ -1363,32 +1391,39 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
     const float* Pr = s.P + rr * s.ld_P + M;
     const float* PsT = s.P + (RP + rs) * s.ld_P;
     const float* PrT = s.P + (RP + rr) * s.ld_P + M;
-    static_for<NF>([&](auto Fc) {
-      constexpr int fb = decltype(Fc)::value;
-      static_for<4>([&](auto Qc) {
-        constexpr int q = decltype(Qc)::value;
-        const int row = fb * 32 + 8 * q + 4 * kk;
-        const f32x4 w = *reinterpret_cast<const f32x4*>(s.vecs + (2 * L - 1) * (NF * 32) + row);
-        const f32x4 ps = *reinterpret_cast<const f32x4*>(Ps + row);
-        const f32x4 pr = *reinterpret_cast<const f32x4*>(Pr + row);
-        const f32x4 pst = *reinterpret_cast<const f32x4*>(PsT + row);
-        const f32x4 prt = *reinterpret_cast<const f32x4*>(PrT + row);
-        static_for<2>([&](auto Hc) {
-          constexpr int e = 2 * decltype(Hc)::value;
-          float y[2], d[2];
+    // as the primal split kernels: one round of 4 features per fenced step, the next round's 5 reads issued first
+    constexpr int NQ = 4 * NF;
+    auto rd5 = [&](int q, f32x4 (&o)[5]) {
+      const int row = (q >> 2) * 32 + 8 * (q & 3) + 4 * kk;
+      o[0] = *reinterpret_cast<const f32x4*>(s.vecs + (2 * L - 1) * (NF * 32) + row);
+      o[1] = *reinterpret_cast<const f32x4*>(Ps + row);
+      o[2] = *reinterpret_cast<const f32x4*>(Pr + row);
+      o[3] = *reinterpret_cast<const f32x4*>(PsT + row);
+      o[4] = *reinterpret_cast<const f32x4*>(PrT + row);
+    };
+    f32x4 lb[2][5];
+    rd5(0, lb[0]);
+    static_for<NQ>([&](auto Qc) {
+      constexpr int q = decltype(Qc)::value, fb = q >> 2, qq = q & 3;
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (q + 1 < NQ) rd5(q + 1, lb[(q + 1) & 1]);
+      const f32x4(&o)[5] = lb[q & 1];
+      static_for<2>([&](auto Hc) {
+        constexpr int e = 2 * decltype(Hc)::value;
+        float y[2], d[2];
 #pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const float u = ps[e + h] + pr[e + h] + len2 * w[e + h];
-            const float du = pst[e + h] + prt[e + h] + dlen2 * w[e + h];
-            const float r = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(u));
-            y[h] = u * r;
-            d[h] = r * du * fmaf(u - y[h], kNegLn2, 1.0f);
-          }
-          put_pair<NF, fb, 4 * q + e>(XA, y[0], y[1]);
-          put_pair<NF, fb, 4 * q + e>(XAT, d[0], d[1]);
-        });
+        for (int h = 0; h < 2; ++h) {
+          const float u = o[1][e + h] + o[2][e + h] + len2 * o[0][e + h];
+          const float du = o[3][e + h] + o[4][e + h] + dlen2 * o[0][e + h];
+          const float r = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(u));
+          y[h] = u * r;
+          d[h] = r * du * fmaf(u - y[h], kNegLn2, 1.0f);
+        }
+        put_pair<NF, fb, 4 * qq + e>(XA, y[0], y[1]);
+        put_pair<NF, fb, 4 * qq + e>(XAT, d[0], d[1]);
       });
     });
+    __builtin_amdgcn_sched_barrier(0);
     STAMP_LANE0(s, kStEdgeLayer1, t_sub);
     ChainInv ie, ix;
     static_for<2 * 4 - 1>([&](auto Lc) {
@@ -1755,16 +1790,10 @@ __device__ __forceinline__ void edge_tile_cols(const Net& net, const BlockW& bw,
   sc.init(valid ? rr : -1, li);
   const bool writer = valid && sc.tail;
   if (agg) {
-    // gate e_ij = sigmoid(m_ij . w_g + b_g) over every block, in edge_tail's order (egnn.py:99-101)
-    float part = 0.f;
-#pragma unroll
-    for (int fb = 0; fb < NF; ++fb)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const f32x4 w = *reinterpret_cast<const f32x4*>(s.vecs + (2 * L) * (NF * 32) + fb * 32 + 8 * q + 4 * kk);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) part += w[e] * m[fb][4 * q + e];
-      }
+    // gate e_ij = sigmoid(m_ij . w_g + b_g) over every block, edge_tail's lds_dot (the same summation order: cols
+    // results stay bitwise the batch path's; egnn.py:99-101)
+    float part, partT;
+    lds_dot<NF, 0>(s.vecs + (2 * L) * (NF * 32), m, m, kk, part, partT);
     part += __shfl_xor(part, 32);
     const float g = sigmoidf_(part + bw.bg);
     // this wave's message blocks: scatter_sum(m_ij e_ij) (egnn.py:102-104), segment parts stored as edge_tail does
