@@ -177,6 +177,67 @@ __global__ __launch_bounds__(kLseThreads) void lse_partials_kernel(const float* 
   if (tid < 7) out[tid] = red[tid][0];
 }
 
+// Re-deal of a chunked adaptive solve (integrate_impl): the molecules still unfinished after the first chunk
+// (SolverState kSsActive), ordered by their estimated remaining steps (tau1 - tau) / dt, longest first (ties in batch
+// order), into order[0 .. *nslots).  The next launch resumes them in that order: with more workgroups than CUs, the
+// workgroups start in dispatch order as CUs free up, and a long solve dealt late finishes late (ALDP B = 512 PID
+// log_prob: 55.5 ms in batch order, 37.9 ms with the molecules sorted by their step counts; the slowest molecule alone
+// 36.8 ms).  One workgroup, bitonic sort of (key, index) in LDS.
+constexpr int kRedealMax = 4096;
+constexpr int kRedealThreads = 1024;
+// step controls of a re-dealt solve's first launch (sched_floats).  ALDP B = 512 PID log_prob (tools/diag/
+// redeal_keys.py, sched_check.py): after 2 / 4 / 8 steps the (tau1 - tau) / dt order ranks the remaining NFE at
+// Spearman 0.29 / 0.53 / 0.82 and the launch takes 51.8 / 44.3 / 43.9 ms (one launch: 55.3); at 8 the second launch's
+// makespan equals that of the true remaining-NFE order, the rest is the first launch's two rounds of 512 workgroups
+constexpr int kChunkSteps = 8;
+
+__global__ __launch_bounds__(kRedealThreads) void redeal_kernel(const float* __restrict__ state, int stride, int ND,
+                                                                int B, float tau1, int* order, int* nslots) {
+  __shared__ float key[kRedealMax];
+  __shared__ int idx[kRedealMax];
+  const int tid = threadIdx.x;
+  int n2 = 1;
+  while (n2 < B) n2 <<= 1;
+  for (int i = tid; i < n2; i += kRedealThreads) {
+    float k = -INFINITY;   // finished molecules and padding sort last
+    if (i < B) {
+      const float* S = state + (size_t)i * stride + 2 * ND;
+      if (__builtin_bit_cast(int, S[kSsActive])) {
+        const float r = (tau1 - S[kSsTau]) / S[kSsDt];
+        k = r >= 0.f ? fminf(r, 3.0e38f) : (r < 0.f ? 0.f : 3.0e38f);   // a NaN estimate (non-finite step) first
+      }
+    }
+    key[i] = k;
+    idx[i] = i;
+  }
+  __syncthreads();
+  // bitonic sort into "before" order: larger key first, then smaller index (a strict total order)
+  for (int size = 2; size <= n2; size <<= 1)
+    for (int half = size >> 1; half > 0; half >>= 1) {
+      for (int i = tid; i < n2; i += kRedealThreads) {
+        const int j = i ^ half;
+        if (j > i) {
+          const float ki = key[i], kj = key[j];
+          const int ii = idx[i], ij = idx[j];
+          const bool j_before = kj > ki || (kj == ki && ij < ii);
+          if (((i & size) == 0) == j_before) {
+            key[i] = kj;
+            key[j] = ki;
+            idx[i] = ij;
+            idx[j] = ii;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  for (int i = tid; i < B; i += kRedealThreads) {
+    if (!(key[i] > -INFINITY)) continue;
+    order[i] = idx[i];
+    if (i + 1 == B || !(key[i + 1] > -INFINITY)) *nslots = i + 1;
+  }
+  if (tid == 0 && !(key[0] > -INFINITY)) *nslots = 0;
+}
+
 }  // namespace ecnf
 
 // =====================================================================================================
@@ -511,6 +572,8 @@ bool shape_supported(const ecnf_cfg& c, int NT, int P = -1) {
 // penalty per extra molecule for the expected max of m step counts (0: measured on ALDP B = 512 PID, penalty
 // 0 / 0.15 / 0.3 -> sample 3.23 / 3.73 / 3.70 ms, Hutchinson log_prob 57.9 / 58.0 / 58.1 ms,
 // profiles/round2/mpw_ab.log).
+// (Round 5: the M = 64 tangent kernels run one molecule per workgroup anyway (MPW = 1, LDS); their tail is the
+// dispatch order of the workgroups beyond the CU count, which the re-dealt solve addresses, redeal_kernel.)
 constexpr double adaptive_penalty() { return 0.0; }
 
 Net net_for_batch(const ecnf_handle* h, int ix, int B, size_t* lds, bool adaptive = false) {
@@ -589,7 +652,7 @@ int team_size(const ecnf_handle* h, int NT, int B, int* cols, int mode) {
 // G, cols: team_size's decision for this solve (G = 1: the batch path)
 hipError_t dispatch_integrate(const ecnf_handle* h, int NT, const SolveP& sp_in, int G, int cols, const float* y0,
                               const int32_t* feat, const float* eps, float* y1, float* dlogp, int32_t* nfe,
-                              int32_t* status, int B, hipStream_t stream) {
+                              int32_t* status, int B, hipStream_t stream, float* sched = nullptr) {
   const int M = h->cfg.mlp_width, L = h->cfg.mlp_depth, D = h->cfg.dim, P = h->prec, ix = 2 * P + NT;
   size_t lds = 0;
   SolveP sp = sp_in;
@@ -616,8 +679,9 @@ hipError_t dispatch_integrate(const ecnf_handle* h, int NT, const SolveP& sp_in,
     sp.team = TeamP{};
     net = net_for_batch(h, ix, B, &lds, sp.adaptive != 0);
   }
+  auto launch = [&](const SolveP& spl) -> hipError_t {
 #define ECNF_CALL(m, l, d, nt, p) \
-  launch_integrate<m / 32, nt, l, d, p>(net, lds, sp, y0, feat, eps, y1, dlogp, nfe, status, B, stream)
+  launch_integrate<m / 32, nt, l, d, p>(net, lds, spl, y0, feat, eps, y1, dlogp, nfe, status, B, stream)
 #define X(m, l, d)                                                                                           \
   if (M == m && L == l && D == d)                                                                            \
     return NT ? (P ? ECNF_CALL(m, l, d, 1, 1) : ECNF_CALL(m, l, d, 1, 0)) : (P ? ECNF_CALL(m, l, d, 0, 1) : ECNF_CALL(m, l, d, 0, 0));
@@ -629,7 +693,31 @@ hipError_t dispatch_integrate(const ecnf_handle* h, int NT, const SolveP& sp_in,
   ECNF_SHAPES_WIDE_TAN(X)
 #undef X
 #undef ECNF_CALL
-  return hipErrorInvalidValue;
+    return hipErrorInvalidValue;
+  };
+  const int grid = (B + net.MPW - 1) / net.MPW;
+  if (!(sched && G == 1 && sp.adaptive && grid > h->ncu && chunkable(M / 32, NT, P))) return launch(sp);
+  // chunked, re-dealt solve (sched_floats, redeal_kernel)
+  const int ND = h->cfg.n_nodes * h->cfg.dim, stride = solver_state_stride(ND);
+  int* order = reinterpret_cast<int*>(sched + (size_t)B * stride);
+  int* nslots = order + align4(B);
+  SolveP s1 = sp;
+  s1.state = sched;
+  s1.state_stride = stride;
+  s1.chunk_steps = kChunkSteps;
+  hipError_t e = launch(s1);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(redeal_kernel, dim3(1), dim3(kRedealThreads), 0, stream, sched, stride, ND, B, sp.tau1, order,
+                     nslots);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  SolveP s2 = sp;
+  s2.state = sched;
+  s2.state_stride = stride;
+  s2.resume = 1;
+  s2.order = order;
+  s2.nslots = nslots;
+  return launch(s2);
 }
 
 hipError_t dispatch_vf(const ecnf_handle* h, int NT, const float* x, const float* t, const int32_t* feat,
@@ -686,6 +774,19 @@ size_t pcache_stride(const ecnf_handle* h) {
 // slots of a batch: the grid covers ceil(B / m) m <= B + MPW - 1 molecule slots (m <= MPW, net_for_batch)
 size_t pcache_floats(const ecnf_handle* h, int batch) {
   return (size_t)(batch + h->net[2 * h->prec + 1].MPW) * pcache_stride(h);
+}
+
+// Chunked, re-dealt adaptive solves (redeal_kernel): the first launch runs every molecule for kChunkSteps step
+// controls and stores its solver state; the second resumes the unfinished ones, longest estimated remainder first.
+// Results are bitwise those of one launch (a molecule's arithmetic does not depend on its slot or workgroup, and the
+// state crosses the launches exactly).  Taken when the grid has more workgroups than the device has CUs and the
+// caller's workspace (or the handle's arena) holds the scratch below.
+// floats of the re-deal scratch of a solve (0: never re-dealt): [B][solver_state_stride] states, the slot order and
+// the slot count; it follows the exact trace's pcache in the workspace
+size_t sched_floats(const ecnf_handle* h, const ecnf_solve_opts* o, int batch) {
+  if (o->solver != ECNF_SOLVER_DOPRI5 || o->dt0 > 0.f || batch < 2 || batch > kRedealMax) return 0;
+  const int ND = h->cfg.n_nodes * h->cfg.dim;
+  return (size_t)batch * solver_state_stride(ND) + align4(batch) + 4;
 }
 
 int integrate_impl(ecnf_handle* h, const ecnf_solve_opts* o, const float* y0, const int32_t* feat, const float* eps,
@@ -1152,7 +1253,7 @@ int ecnf_vf_jvp(ecnf_handle* h, const float* x, const float* t, const int32_t* f
 int ecnf_integrate_workspace_size(ecnf_handle* h, const ecnf_solve_opts* o, int32_t batch, size_t* bytes) {
   if (!h || !o || !bytes) return fail(ECNF_E_INVALID, "NULL argument");
   if (batch < 0) return fail(ECNF_E_INVALID, "batch < 0");
-  *bytes = exact_sparse(h, o->divergence) ? pcache_floats(h, batch) * sizeof(float) : 0;
+  *bytes = ((exact_sparse(h, o->divergence) ? pcache_floats(h, batch) : 0) + sched_floats(h, o, batch)) * sizeof(float);
   return ECNF_OK;
 }
 
@@ -1254,14 +1355,21 @@ int integrate_impl(ecnf_handle* h, const ecnf_solve_opts* o, const float* y0, co
   sp.pcache = nullptr;
   sp.pcache_slots = 0;
   sp.team = TeamP{};   // dispatch_integrate sets it (team_size)
+  sp.order = nullptr;
+  sp.nslots = nullptr;
+  sp.state = nullptr;
+  sp.state_stride = 0;
+  sp.chunk_steps = 0;
+  sp.resume = 0;
   // team mode decided once for this solve: one read of the handle's mode (ecnf_set_team may run concurrently)
   int cols = 0;
   const int G = team_size(h, NT, batch, &cols, h->team_mode.load());
   const size_t need = sp.sparse1 ? pcache_floats(h, batch) : 0;
+  const size_t need_s = G == 1 ? sched_floats(h, o, batch) : 0;
   // the arena pointer and size are read under arena_mu, and the lock is held through the dispatch that uses them:
   // an ecnf_reserve_workspace on another thread cannot free the arena between the read and the launch
   std::unique_lock<std::mutex> lk(h->arena_mu, std::defer_lock);
-  if (arena && need) {
+  if (arena && (need || need_s)) {
     lk.lock();
     ws = h->arena;
     ws_bytes = h->arena_bytes;
@@ -1269,16 +1377,18 @@ int integrate_impl(ecnf_handle* h, const ecnf_solve_opts* o, const float* y0, co
   const bool cached = sp.sparse1 && h->exact_form == ECNF_EXACT_FORM_DEFAULT && ws && ws_bytes >= need * sizeof(float);
   if (cached) {
     sp.pcache = ws;
-    sp.pcache_slots = (int)(ws_bytes / sizeof(float) / pcache_stride(h));
+    sp.pcache_slots = (int)(need / pcache_stride(h));
   }
+  // the re-deal scratch follows the pcache region (a workspace too small for both runs the solve in one launch)
+  float* sched = need_s && ws && ws_bytes >= (need + need_s) * sizeof(float) ? ws + need : nullptr;
   HIP_TRY(hipSetDevice(h->device));
-  if (cached && arena) {
+  if ((cached || sched) && arena) {
     // the arena is shared by every ecnf_integrate call on the handle: calls on different streams are ordered
     // through an event (no host synchronisation), and the bookkeeping is guarded for calls from several threads
     // (arena_mu, held since the arena was read)
     if (!h->arena_ev) HIP_TRY(hipEventCreateWithFlags(&h->arena_ev, hipEventDisableTiming));
     if (h->arena_used && h->arena_stream != stream) HIP_TRY(hipStreamWaitEvent(stream, h->arena_ev, 0));
-    HIP_TRY(dispatch_integrate(h, NT, sp, G, cols, y0, feat, eps, y1, dlogp, nfe, status, batch, stream));
+    HIP_TRY(dispatch_integrate(h, NT, sp, G, cols, y0, feat, eps, y1, dlogp, nfe, status, batch, stream, sched));
     HIP_TRY(hipEventRecord(h->arena_ev, stream));
     h->arena_used = true;
     h->arena_stream = stream;
@@ -1292,7 +1402,7 @@ int integrate_impl(ecnf_handle* h, const ecnf_solve_opts* o, const float* y0, co
     h->team_used = true;
     h->team_stream = stream;
   } else {
-    HIP_TRY(dispatch_integrate(h, NT, sp, G, cols, y0, feat, eps, y1, dlogp, nfe, status, batch, stream));
+    HIP_TRY(dispatch_integrate(h, NT, sp, G, cols, y0, feat, eps, y1, dlogp, nfe, status, batch, stream, sched));
   }
   g_err.clear();
   return ECNF_OK;

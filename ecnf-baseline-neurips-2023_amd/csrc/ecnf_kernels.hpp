@@ -52,7 +52,27 @@ struct SolveP {
   // team (latency) mode of the primal kernels (egnn_eval.hpp team_exchange): team.G > 1 workgroups per molecule,
   // MPW = 1, grid = batch x G (a cooperative launch: every member co-resident)
   TeamP team;
+  // re-dealt adaptive solves (ecnf_hip.hip integrate_impl): `order` maps launch slots to batch molecules (nullptr:
+  // the identity) and *nslots (device memory) is the number of occupied slots (nullptr: B); `state` [B][state_stride]
+  // holds a molecule's solver state at a step boundary (SolverState), stored when the launch stops after
+  // `chunk_steps` > 0 step controls (or ends) and loaded instead of the initial state when `resume` is set
+  const int* order;
+  const int* nslots;
+  float* state;
+  int state_stride, chunk_steps, resume;
 };
+
+// one molecule's solver state at a step boundary (stage 1 of the next step, FSAL k1 in kx[0]): y [ND], k1 [ND], then
+// these scalars (ints as their bits)
+enum SolverState { kSsLp = 0, kSsKl, kSsTau, kSsDt, kSsTnext, kSsAtmin, kSsNfe, kSsSteps, kSsStatus, kSsActive, kSsCount };
+__host__ __device__ inline int solver_state_stride(int ND) { return align4(2 * ND + kSsCount); }
+// batch molecule of launch slot slot0 + m (re-dealt solves: through the slot order)
+__device__ __forceinline__ int mol_index(const int* order, int slot0, int m) {
+  return order ? order[slot0 + m] : slot0 + m;
+}
+// kernels that can stop and resume (every integrate kernel but the strict-fp32 M = 256 tangent one, whose 92 spilled
+// registers crash the compiler's AGPR-copy rewrite pass once the state copies are added; its solves run in one launch)
+__host__ __device__ constexpr bool chunkable(int NF, int NT, int P) { return !(P == 1 && NF == 8 && NT == 1); }
 
 // solver state in LDS, after the eval region
 struct SolverLds {
@@ -208,8 +228,10 @@ __global__ __launch_bounds__((kernel_threads<NF, NT, P, COLS>())) __attribute__(
   const TeamCtx* tm = team ? &team_ctx : nullptr;
   int tepoch = 0;
   const bool writer_wg = team_ctx.r == 0;
-  const int mol0 = team ? team_ctx.T : (int)blockIdx.x * MPW;
-  const int nmol = min(MPW, B - mol0);
+  // launch slots slot0 .. slot0 + nmol - 1; slot j integrates batch molecule sp.order[j] (re-dealt solves) or j
+  const int slot0 = team ? team_ctx.T : (int)blockIdx.x * MPW;
+  const int nmol = min(MPW, (sp.nslots ? *sp.nslots : B) - slot0);
+  if (nmol <= 0) return;   // a re-dealt launch keeps the batch's grid; slots past the unfinished molecules are empty
   ECNF_DCHECK((int)(s.tail - smem) + solver_lds_floats(MPW, ND) <= net.lds_floats, 0);
   ECNF_DCHECK(nmol >= 1 && nmol <= MPW, 5);
 
@@ -218,10 +240,14 @@ __global__ __launch_bounds__((kernel_threads<NF, NT, P, COLS>())) __attribute__(
   __syncthreads();
   for (int i = tid; i < MPW * ND; i += kThreads) {
     const int m = i / ND;
-    st.y[i] = m < nmol ? y0[(size_t)mol0 * ND + i] : 0.f;
-    st.eps[i] = (m < nmol && eps) ? eps[(size_t)mol0 * ND + i] : 0.f;
+    const size_t g = m < nmol ? (size_t)mol_index(sp.order, slot0, m) * ND + (i - m * ND) : 0;
+    st.y[i] = m < nmol ? y0[g] : 0.f;
+    st.eps[i] = (m < nmol && eps) ? eps[g] : 0.f;
   }
-  for (int i = tid; i < MPW * N; i += kThreads) s.feat[i] = (i / N) < nmol ? feat[(size_t)mol0 * N + i] : 0;
+  for (int i = tid; i < MPW * N; i += kThreads) {
+    const int m = i / N;
+    s.feat[i] = m < nmol ? feat[(size_t)mol_index(sp.order, slot0, m) * N + (i - m * N)] : 0;
+  }
   if (tid < MPW) {
     st.lp[tid] = 0.f;
     st.tau[tid] = sp.tau0;
@@ -243,6 +269,32 @@ __global__ __launch_bounds__((kernel_threads<NF, NT, P, COLS>())) __attribute__(
     st.ctl[2] = 0;
     st.ctl[3] = sp.solver == ECNF_SOLVER_EULER ? kEuler : (sp.adaptive ? kInit0 : kFsal);
     st.ctl[4] = 1;
+    st.ctl[5] = 0;   // step controls in this launch (chunked solves)
+    if (chunkable(NF, NT, P) && sp.resume) {   // a resumed molecule continues at stage 1 of its next step
+      st.ctl[3] = kStage;
+      st.ctl[4] = 1;
+    }
+  }
+  if (chunkable(NF, NT, P) && sp.resume) {
+    for (int i = tid; i < nmol * ND; i += kThreads) {
+      const int m = i / ND, c = i - m * ND;
+      const float* S = sp.state + (size_t)mol_index(sp.order, slot0, m) * sp.state_stride;
+      st.y[i] = S[c];
+      st.kx[i] = S[ND + c];
+    }
+    if (tid < nmol) {
+      const float* S = sp.state + (size_t)mol_index(sp.order, slot0, tid) * sp.state_stride + 2 * ND;
+      st.lp[tid] = S[kSsLp];
+      st.kl[tid] = S[kSsKl];
+      st.tau[tid] = S[kSsTau];
+      st.dt[tid] = S[kSsDt];
+      st.tnext[tid] = S[kSsTnext];
+      st.atmin[tid] = __builtin_bit_cast(int, S[kSsAtmin]);
+      st.nfe[tid] = __builtin_bit_cast(int, S[kSsNfe]);
+      st.steps[tid] = __builtin_bit_cast(int, S[kSsSteps]);
+      st.status[tid] = __builtin_bit_cast(int, S[kSsStatus]);
+      st.active[tid] = __builtin_bit_cast(int, S[kSsActive]);
+    }
   }
   __syncthreads();
   // device-side input check (no host sync on the call path): a molecule with an embedding id outside
@@ -298,6 +350,9 @@ __global__ __launch_bounds__((kernel_threads<NF, NT, P, COLS>())) __attribute__(
         if (tid < MPW) st.h[tid] = st.tnext[tid] - st.tau[tid];
         __syncthreads();
         if (*st.any == 0) break;
+        // chunked solve: stop at this step boundary once the launch has done its step controls (state stored below)
+        const int chunk = chunkable(NF, NT, P) ? opaque_u(sp.chunk_steps) : 0;
+        if (chunk > 0 && __builtin_amdgcn_readfirstlane(st.ctl[5]) >= chunk) break;
       }
       for (int i = tid; i < MPW * ND; i += kThreads) {
         float acc = 0.f;
@@ -442,6 +497,7 @@ __global__ __launch_bounds__((kernel_threads<NF, NT, P, COLS>())) __attribute__(
         }
       }
       stage = 1;
+      if (tid == 0) st.ctl[5] += 1;
     }
     if (tid == 0) {   // the control state of the next trip (read by every thread after the barrier)
       st.ctl[0] = __builtin_bit_cast(int, e_tau);
@@ -469,6 +525,28 @@ __global__ __launch_bounds__((kernel_threads<NF, NT, P, COLS>())) __attribute__(
   {
   const int tid = opaque_tid();
   const SolverLds st = carve_solver(smem + solver_size(2), MPW, ND);
+  if (chunkable(NF, NT, P) && sp.chunk_steps > 0) {   // chunked solve: every molecule's state at this step boundary
+    for (int i = tid; i < nmol * ND; i += kThreads) {
+      const int m = i / ND, c = i - m * ND;
+      float* S = sp.state + (size_t)mol_index(sp.order, slot0, m) * sp.state_stride;
+      S[c] = st.y[i];
+      S[ND + c] = st.kx[i];
+    }
+    if (tid < nmol) {
+      float* S = sp.state + (size_t)mol_index(sp.order, slot0, tid) * sp.state_stride + 2 * ND;
+      S[kSsLp] = st.lp[tid];
+      S[kSsKl] = st.kl[tid];
+      S[kSsTau] = st.tau[tid];
+      S[kSsDt] = st.dt[tid];
+      S[kSsTnext] = st.tnext[tid];
+      S[kSsAtmin] = __builtin_bit_cast(float, st.atmin[tid]);
+      S[kSsNfe] = __builtin_bit_cast(float, st.nfe[tid]);
+      S[kSsSteps] = __builtin_bit_cast(float, st.steps[tid]);
+      S[kSsStatus] = __builtin_bit_cast(float, st.status[tid]);
+      S[kSsActive] = __builtin_bit_cast(float, st.active[tid]);
+    }
+    __syncthreads();
+  }
   if (tid < nmol && st.status[tid] == ECNF_OK) {
     bool fin = isfinite(st.lp[tid]);
     for (int c = 0; c < ND; ++c) fin = fin && isfinite(st.y[tid * ND + c]);
@@ -482,11 +560,16 @@ __global__ __launch_bounds__((kernel_threads<NF, NT, P, COLS>())) __attribute__(
     __syncthreads();
     if (!writer_wg) return;
   }
-  for (int i = tid; i < nmol * ND; i += kThreads) y1[(size_t)mol0 * ND + i] = st.y[i];
+  // (a molecule still unfinished at a chunk's end gets provisional outputs, overwritten by the launch that ends it)
+  for (int i = tid; i < nmol * ND; i += kThreads) {
+    const int m = i / ND;
+    y1[(size_t)mol_index(sp.order, slot0, m) * ND + (i - m * ND)] = st.y[i];
+  }
   if (tid < nmol) {
-    if (dlogp) dlogp[mol0 + tid] = st.lp[tid];
-    if (nfe_out) nfe_out[mol0 + tid] = st.nfe[tid];
-    if (status_out) status_out[mol0 + tid] = st.status[tid];
+    const int bm = mol_index(sp.order, slot0, tid);
+    if (dlogp) dlogp[bm] = st.lp[tid];
+    if (nfe_out) nfe_out[bm] = st.nfe[tid];
+    if (status_out) status_out[bm] = st.status[tid];
   }
   }
 }

@@ -221,7 +221,9 @@ class EcnfHandle:
 
     def integrate(self, y0, feat, t0: float, t1: float, opts: SolveOptions, divergence: int = _lib.DIV_NONE,
                   eps=None, check_status: bool = True, fallback: bool = True):
-        """One-launch ODE solve for the whole batch.  Returns (y1, dlogp or None, nfe, status).
+        """ODE solve of the whole batch in one launch (adaptive solves with more workgroups than CUs: two launches,
+        the unfinished molecules re-dealt longest first; bitwise the same results).  Returns (y1, dlogp or None, nfe,
+        status).
 
         check_status: read the per-molecule status back (one sync) and raise like diffrax / chex would:
         ECNF_E_MAX_STEPS -> RuntimeError, ECNF_E_INVALID (embedding ids out of range) -> ValueError.
@@ -277,9 +279,9 @@ class EcnfHandle:
         nfe = torch.empty(B, device=self.device, dtype=torch.int32)
         status = torch.empty(B, device=self.device, dtype=torch.int32)
         o = opts.to_c(t0, t1, divergence)
-        # the exact trace's primal-aggregate cache: a caller-owned workspace from torch's stream-ordered caching
-        # allocator (ecnf_integrate_ws), so concurrent solves on one handle never share it and the call allocates
-        # nothing itself
+        # the exact trace's primal-aggregate cache and the adaptive solves' re-deal scratch: a caller-owned workspace
+        # from torch's stream-ordered caching allocator (ecnf_integrate_ws), so concurrent solves on one handle never
+        # share it and the call allocates nothing itself
         nbytes = ctypes.c_size_t(0)
         _lib.check(self.lib.ecnf_integrate_workspace_size(self._h, ctypes.byref(o), B, ctypes.byref(nbytes)))
         ws = torch.empty(nbytes.value, device=self.device, dtype=torch.uint8) if nbytes.value else None

@@ -128,6 +128,11 @@ int ecnf_integrate(ecnf_handle* h, const ecnf_solve_opts* opts, const float* y0,
  * primal is the same; with a workspace, the first pass caches the primal edge aggregates of the blocks whose edge
  * tangents are sparse (blocks 1 and K) and the later passes skip those primal tiles.  Results are bitwise equal with
  * and without a workspace; only the time differs (LJ13 B = 1024 Euler-100 log_prob: ~1.35 s vs ~1.75 s).
+ * Adaptive (Dopri5 + PID) solves of 2 .. 4096 molecules also use it, after the exact trace's cache, for the re-deal
+ * scratch: when the batch needs more workgroups than the device has CUs, a first launch runs every molecule for a
+ * few steps and stores its solver state, and a second launch resumes the unfinished molecules longest estimated
+ * remainder first, so the slow molecules do not start late in dispatch order (ALDP B = 512 PID log_prob: ~44 ms vs
+ * ~55 ms).  Bitwise the same results; a workspace too small for both regions runs the solve in one launch.
  *   ecnf_integrate_workspace_size  bytes a call with these options and batch needs (0: none is used)
  *   ecnf_integrate_ws              ecnf_integrate with a CALLER-owned device workspace (NULL: none); the workspace is
  *                                  used stream-ordered on `stream` only, so concurrent calls with distinct
