@@ -1,5 +1,5 @@
 """Summarise tools/profile_configs.sh output: per case, the bench line (HIP-event ms per launch), the rocprofv3 kernel
-trace average of integrate_kernel, and the counter passes (HBM bytes per launch = 2 x FETCH_SIZE + WRITE_SIZE with the
+trace average of integrate_kernel (per solve: a re-dealt adaptive solve is two launches), and the counter passes (HBM bytes per launch = 2 x FETCH_SIZE + WRITE_SIZE with the
 gfx950 16-B/lane FETCH_SIZE correction, effective clock = GRBM_GUI_ACTIVE / 8 XCDs / duration, MFMA pipe busy =
 SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs)).  Usage: python tools/pmc_configs.py PROFILE_DIR"""
 import csv
@@ -38,21 +38,31 @@ def main(prof):
             line = json.loads(open(os.path.join(d, "line_kt.json")).read().strip().splitlines()[-1])
         except (OSError, ValueError, IndexError):
             continue
-        stats = [r for r in rows(os.path.join(d, "kt", "**", "*kernel_stats.csv")) if "integrate_kernel" in r["Name"]]
-        kt_avg_ms = float(stats[0]["AverageNs"]) * 1e-6 if stats else None
+        allstats = rows(os.path.join(d, "kt", "**", "*kernel_stats.csv"))
+        stats = [r for r in allstats if "integrate_kernel" in r["Name"]]
+        # a re-dealt adaptive solve (ecnf_hip.hip redeal_kernel) is two integrate launches: every per-launch figure
+        # below is per SOLVE, summed over its launches
+        per = 2 if any("redeal_kernel" in r["Name"] for r in allstats) else 1
+        kt_avg_ms = float(stats[0]["AverageNs"]) * 1e-6 * per if stats else None
         rec = {"case": case, "bench_ms": line["ms"], "tflops": line["tflops"], "nfe_mean": line["nfe_mean"],
-               "rocprof_avg_ms": kt_avg_ms, "rocprof_calls": int(stats[0]["Calls"]) if stats else None,
-               "frac_of_split_peak": line["tflops"] / PEAK_SPLIT}
+               "rocprof_avg_ms": kt_avg_ms, "rocprof_calls": int(stats[0]["Calls"]) // per if stats else None,
+               "launches_per_solve": per, "frac_of_split_peak": line["tflops"] / PEAK_SPLIT}
         c0, d0 = per_dispatch(os.path.join(d, "p0"))
         c1, _ = per_dispatch(os.path.join(d, "p1"))
         if c0 and c1:
-            k0 = sorted(c0)[1:] or sorted(c0)     # drop the warm-up dispatch
-            k1 = sorted(c1)[1:] or sorted(c1)
-            fetch = statistics.median(c0[k]["FETCH_SIZE"] for k in k0)
-            gui = statistics.median(c0[k]["GRBM_GUI_ACTIVE"] for k in k0)
-            busy = statistics.median(c0[k]["SQ_VALU_MFMA_BUSY_CYCLES"] for k in k0)
-            write = statistics.median(c1[k]["WRITE_SIZE"] for k in k1)
-            dur = statistics.median(d0[k] for k in k0 if k in d0) if d0 else None
+            def solves(c, dd=None):
+                ks = sorted(c)
+                groups = [ks[i:i + per] for i in range(0, len(ks) - per + 1, per)]
+                groups = groups[1:] or groups     # drop the warm-up solve
+                return [({n: sum(c[k][n] for k in g) for n in c[g[0]]},
+                         sum(dd[k] for k in g) if dd and all(k in dd for k in g) else None) for g in groups]
+            s0, s1 = solves(c0, d0), solves(c1)
+            fetch = statistics.median(v["FETCH_SIZE"] for v, _ in s0)
+            gui = statistics.median(v["GRBM_GUI_ACTIVE"] for v, _ in s0)
+            busy = statistics.median(v["SQ_VALU_MFMA_BUSY_CYCLES"] for v, _ in s0)
+            write = statistics.median(v["WRITE_SIZE"] for v, _ in s1)
+            durs = [t for _, t in s0 if t]
+            dur = statistics.median(durs) if durs else None
             rec.update({"hbm_bytes_per_launch": (2 * fetch + write) * 1024, "fetch_size_kib_raw": fetch,
                         "write_size_kib": write, "grbm_gui_active": gui,
                         "clock_ghz_grbm": gui / 8 / (dur * 1e-9) / 1e9 if dur else None,
