@@ -19,9 +19,9 @@ if not torch.cuda.is_available():
     pytest.skip("needs a ROCm GPU", allow_module_level=True)
 
 
-def _solve(h, x0, feat, eps, t0, t1, div, workspace):
+def _solve(h, x0, feat, eps, t0, t1, div, workspace, max_steps=4096):
     B = x0.shape[0]
-    o = SolveOptions("dopri5", None).to_c(t0, t1, div)
+    o = SolveOptions("dopri5", None, max_steps=max_steps).to_c(t0, t1, div)
     nbytes = ctypes.c_size_t(0)
     _lib.check(h.lib.ecnf_integrate_workspace_size(h._h, ctypes.byref(o), B, ctypes.byref(nbytes)))
     ws = torch.empty(nbytes.value, device="cuda", dtype=torch.uint8) if (workspace and nbytes.value) else None
@@ -63,6 +63,33 @@ def test_redealt_solve_is_bitwise_the_one_launch_solve(name, B, div):
     # the engine's call (workspace from the caching allocator) is the re-dealt form
     y, dl, nfe, st = h.integrate(x0, feat, t0, t1, SolveOptions("dopri5", None), div, eps)
     assert torch.equal(y, one[0]) and torch.equal(nfe, one[2])
+    h.close()
+
+
+@pytest.mark.timeout(240)
+def test_redealt_solve_statuses():
+    """Per-molecule statuses through the two launches: molecules that exceed max_steps inside the first launch (4 steps)
+    or the second (12), and molecules with embedding ids out of range (ECNF_E_INVALID, solved with id 0), end
+    bitwise as in one launch."""
+    cfg = CONFIGS["aldp"]
+    h = EcnfHandle(cfg, init_params(cfg, 0), 0)
+    B = 512
+    g = torch.Generator("cuda").manual_seed(11)
+    z = torch.randn((B, cfg.event_dim), device="cuda", generator=g)
+    x0 = h.base_sample(z)
+    feat = (torch.arange(cfg.n_nodes, device="cuda", dtype=torch.int32) % cfg.n_features).expand(B, -1).contiguous()
+    feat[5, 3] = cfg.n_features + 4
+    feat[300, 0] = -1
+    eps = torch.randn((B, cfg.event_dim), device="cuda", generator=g)
+    for max_steps in (4, 12):
+        one = _solve(h, x0, feat, eps, 1.0, 0.0, _lib.DIV_HUTCHINSON, False, max_steps)
+        red = _solve(h, x0, feat, eps, 1.0, 0.0, _lib.DIV_HUTCHINSON, True, max_steps)
+        st = one[3].cpu()
+        # (a molecule that also runs out of steps reports ECNF_E_MAX_STEPS, the later of the two)
+        assert int(st[5]) in (_lib.ECNF_E_INVALID, _lib.ECNF_E_MAX_STEPS) and int(st[300]) != _lib.ECNF_OK
+        assert int((st == _lib.ECNF_E_MAX_STEPS).sum()) > 0
+        for a, b in zip(one[:4], red[:4]):
+            assert torch.equal(a, b)
     h.close()
 
 
