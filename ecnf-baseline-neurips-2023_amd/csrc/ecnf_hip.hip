@@ -182,9 +182,16 @@ __global__ __launch_bounds__(kLseThreads) void lse_partials_kernel(const float* 
 // order), into order[0 .. *nslots).  The next launch resumes them in that order: with more workgroups than CUs, the
 // workgroups start in dispatch order as CUs free up, and a long solve dealt late finishes late (ALDP B = 512 PID
 // log_prob: 55.5 ms in batch order, 37.9 ms with the molecules sorted by their step counts; the slowest molecule alone
-// 36.8 ms).  One workgroup, bitonic sort of (key, index) in LDS.
-constexpr int kRedealMax = 4096;
+// 36.8 ms).  One workgroup, bitonic sort of (key, index): in LDS up to kRedealLds molecules, beyond that in the
+// workspace (gkey / gidx, next power of two entries; one workgroup's global accesses are ordered by its barriers).
+constexpr int kRedealLds = 4096;
+constexpr int kRedealMax = 1 << 20;
 constexpr int kRedealThreads = 1024;
+__host__ __device__ inline int pow2_at_least(int n) {
+  int p = 1;
+  while (p < n) p <<= 1;
+  return p;
+}
 // step controls of a re-dealt solve's first launch (sched_floats).  ALDP B = 512 PID log_prob (tools/diag/
 // redeal_keys.py, sched_check.py): after 2 / 4 / 8 steps the (tau1 - tau) / dt order ranks the remaining NFE at
 // Spearman 0.29 / 0.53 / 0.82 and the launch takes 51.8 / 44.3 / 43.9 ms (one launch: 55.3); at 8 the second launch's
@@ -192,12 +199,14 @@ constexpr int kRedealThreads = 1024;
 constexpr int kChunkSteps = 8;
 
 __global__ __launch_bounds__(kRedealThreads) void redeal_kernel(const float* __restrict__ state, int stride, int ND,
-                                                                int B, float tau1, int* order, int* nslots) {
-  __shared__ float key[kRedealMax];
-  __shared__ int idx[kRedealMax];
+                                                                int B, float tau1, int* order, int* nslots, float* gkey,
+                                                                int* gidx) {
+  __shared__ float lkey[kRedealLds];
+  __shared__ int lidx[kRedealLds];
   const int tid = threadIdx.x;
-  int n2 = 1;
-  while (n2 < B) n2 <<= 1;
+  const int n2 = pow2_at_least(B);
+  float* key = n2 <= kRedealLds ? lkey : gkey;
+  int* idx = n2 <= kRedealLds ? lidx : gidx;
   for (int i = tid; i < n2; i += kRedealThreads) {
     float k = -INFINITY;   // finished molecules and padding sort last
     if (i < B) {
@@ -701,6 +710,8 @@ hipError_t dispatch_integrate(const ecnf_handle* h, int NT, const SolveP& sp_in,
   const int ND = h->cfg.n_nodes * h->cfg.dim, stride = solver_state_stride(ND);
   int* order = reinterpret_cast<int*>(sched + (size_t)B * stride);
   int* nslots = order + align4(B);
+  float* gkey = reinterpret_cast<float*>(nslots + 4);   // the sort's scratch beyond kRedealLds molecules
+  int* gidx = reinterpret_cast<int*>(gkey + pow2_at_least(B));
   SolveP s1 = sp;
   s1.state = sched;
   s1.state_stride = stride;
@@ -708,7 +719,7 @@ hipError_t dispatch_integrate(const ecnf_handle* h, int NT, const SolveP& sp_in,
   hipError_t e = launch(s1);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(redeal_kernel, dim3(1), dim3(kRedealThreads), 0, stream, sched, stride, ND, B, sp.tau1, order,
-                     nslots);
+                     nslots, gkey, gidx);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   SolveP s2 = sp;
@@ -785,8 +796,8 @@ size_t pcache_floats(const ecnf_handle* h, int batch) {
 // the slot count; it follows the exact trace's pcache in the workspace
 size_t sched_floats(const ecnf_handle* h, const ecnf_solve_opts* o, int batch) {
   if (o->solver != ECNF_SOLVER_DOPRI5 || o->dt0 > 0.f || batch < 2 || batch > kRedealMax) return 0;
-  const int ND = h->cfg.n_nodes * h->cfg.dim;
-  return (size_t)batch * solver_state_stride(ND) + align4(batch) + 4;
+  const int ND = h->cfg.n_nodes * h->cfg.dim, n2 = pow2_at_least(batch);
+  return (size_t)batch * solver_state_stride(ND) + align4(batch) + 4 + (n2 > kRedealLds ? 2 * (size_t)n2 : 0);
 }
 
 int integrate_impl(ecnf_handle* h, const ecnf_solve_opts* o, const float* y0, const int32_t* feat, const float* eps,

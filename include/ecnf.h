@@ -128,7 +128,7 @@ int ecnf_integrate(ecnf_handle* h, const ecnf_solve_opts* opts, const float* y0,
  * primal is the same; with a workspace, the first pass caches the primal edge aggregates of the blocks whose edge
  * tangents are sparse (blocks 1 and K) and the later passes skip those primal tiles.  Results are bitwise equal with
  * and without a workspace; only the time differs (LJ13 B = 1024 Euler-100 log_prob: ~1.35 s vs ~1.75 s).
- * Adaptive (Dopri5 + PID) solves of 2 .. 4096 molecules also use it, after the exact trace's cache, for the re-deal
+ * Adaptive (Dopri5 + PID) solves of 2 .. 2^20 molecules also use it, after the exact trace's cache, for the re-deal
  * scratch: when the batch needs more workgroups than the device has CUs, a first launch runs every molecule for a
  * few steps and stores its solver state, and a second launch resumes the unfinished molecules longest estimated
  * remainder first, so the slow molecules do not start late in dispatch order (ALDP B = 512 PID log_prob: ~44 ms vs

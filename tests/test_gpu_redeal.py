@@ -38,7 +38,8 @@ def _solve(h, x0, feat, eps, t0, t1, div, workspace, max_steps=4096):
 
 @pytest.mark.timeout(240)
 @pytest.mark.parametrize("name,B,div", [("aldp", 512, _lib.DIV_HUTCHINSON), ("aldp", 600, _lib.DIV_NONE),
-                                        ("lj13", 1024, _lib.DIV_HUTCHINSON)])
+                                        ("lj13", 1024, _lib.DIV_HUTCHINSON),
+                                        ("aldp", 5000, _lib.DIV_NONE)])   # > 4096: the sort in the workspace
 def test_redealt_solve_is_bitwise_the_one_launch_solve(name, B, div):
     cfg = CONFIGS[name]
     h = EcnfHandle(cfg, init_params(cfg, 0), 0)
