@@ -3,12 +3,11 @@
 1. No data hazard around an inline-asm instruction (tools/isa_hazards.py: the fused DPP segment scans of
    SegScan::sum_fused and the fp16 residual split of split_pair; LLVM's hazard recognizer does not look inside inline
    asm, so these wait states are the source's responsibility).
-2. The message aggregation's LDS atomics stay in the validated flat form.  Round 4 and round 5: every
-   build whose (128, 2, 3) tangent vf_kernel issued the 16-wide macc aggregation as ds_add_f32 returned garbage and then
-   faulted on the GPU (tools/gpu_r5a.sh ... r5e.sh), while the flat_atomic_add_f32 form of the same source is correct;
-   the failure follows the schedule, not the address arithmetic (checked instruction by instruction), and is not
-   explained yet.  A run of 8 or more consecutive ds_add_f32 is that aggregation; the shift sums (dxacc) issue at most
-   2 D per site and are not affected.
+2. The message aggregation's LDS atomics stay in the validated flat form.  Rounds 4 and 5 saw NaN fields
+   and faults in single-shape builds of the (128, 2, 3) tangent vf_kernel, first attributed to the ds_add_f32 form of
+   this aggregation; round 5 found the failing kernel byte-identical to the passing one (flat atomics in both), so the
+   attribution is withdrawn and the failure no longer reproduces, but the form every GPU run since validated is kept.
+   A run of 8 or more consecutive ds_add_f32 is that aggregation; the shift sums (dxacc) issue at most 2 D per site.
 """
 import os
 import re
