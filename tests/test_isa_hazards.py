@@ -5,8 +5,10 @@
    asm, so these wait states are the source's responsibility).
 2. The message aggregation's LDS atomics stay in the validated flat form.  Rounds 4 and 5 saw NaN fields
    and faults in single-shape builds of the (128, 2, 3) tangent vf_kernel, first attributed to the ds_add_f32 form of
-   this aggregation; round 5 found the failing kernel byte-identical to the passing one (flat atomics in both), so the
-   attribution is withdrawn and the failure no longer reproduces, but the form every GPU run since validated is kept.
+   this aggregation; round 5 found that failing build's kernel byte-identical to the passing one (flat atomics in
+   both), but also a current-source reproducer: both aggregation sites of that kernel in ds_add_f32 form return wrong
+   fields (a different value in every process) while either site alone, or both flat, is correct
+   (tools/diag/ds_agg_variants.py).  Not root-caused; the validated flat form is kept.
    A run of 8 or more consecutive ds_add_f32 is that aggregation; the shift sums (dxacc) issue at most 2 D per site.
 """
 import os
