@@ -988,9 +988,9 @@ __device__ __forceinline__ void edge_tail(const Net& net, const BlockW& bw, cons
       } else {
         // per-lane row base through an empty asm: the compiler no longer precomputes (and spills) the 16 lane addresses
         // per block; the atomics compile to flat_atomic_add_f32 on the LDS aperture.  (The same sum through an opaque
-        // integer offset, or the round-3 form, compiles to ds_add_f32, and that build's (128, 2, 3) tangent
-        // vf_kernel returned NaNs / faulted on the GPU (profiles/round4/bisect/); the flat form is the one validated
-        // by the whole GPU suite.)
+        // integer offset compiles to ds_add_f32 — correct in itself — but in the (128, 2, 3) tangent vf_kernel that
+        // form's register allocation hit a compiler miscompile: copies placed before an EXEC restore where EXEC is 0,
+        // DESIGN 5.4, checked on every kernel by tests/test_isa_hazards.py.  The flat form is the validated one.)
         float* mrow = s.macc + rr * s.ld_m + 4 * kk;
         asm volatile("" : "+v"(mrow));
 #pragma unroll

@@ -3,12 +3,19 @@
 1. No data hazard around an inline-asm instruction (tools/isa_hazards.py: the fused DPP segment scans of
    SegScan::sum_fused and the fp16 residual split of split_pair; LLVM's hazard recognizer does not look inside inline
    asm, so these wait states are the source's responsibility).
-2. The message aggregation's LDS atomics stay in the validated flat form.  Rounds 4 and 5 saw NaN fields
-   and faults in single-shape builds of the (128, 2, 3) tangent vf_kernel, first attributed to the ds_add_f32 form of
-   this aggregation; round 5 found that failing build's kernel byte-identical to the passing one (flat atomics in
-   both), but also a current-source reproducer: both aggregation sites of that kernel in ds_add_f32 form return wrong
-   fields (a different value in every process) while either site alone, or both flat, is correct
-   (tools/diag/ds_agg_variants.py).  Not root-caused; the validated flat form is kept.
+2. No vector write where EXEC is zero (tools/isa_exec_copies.py): the cause of the round-4/5 aggregation fault
+   (DESIGN 5.4).  In the failing (128, 2, 3) tangent vf_kernel builds the compiler placed five register-allocation
+   copies (`v_accvgpr_write_b32 a26, v23`, ...) at the head of a loop-exit block that only s_cbranch_execz enters,
+   BEFORE the block's `s_or_b64 exec, exec, s[..]`: with EXEC = 0 they write no lane, and the block loop later reads
+   a26 back (a per-lane value computed at kernel entry), i.e. whatever the previous wave left in the register.
+   Proven on the GPU: the build's results follow the register contents at launch (registers poisoned with 0 / NaN /
+   1.0 give 0.1497849 / NaN / NaN, tools/diag/poison.hip); zeroing register subsets at the kernel entry spells a26
+   (index 282); moving the EXEC restore above the five copies in that build's assembly, nothing else changed, makes
+   every case correct (tools/diag/asm_swap.py asm_ds_fix); and the same ds_add_f32 atomics swapped into the passing
+   build's schedule are correct (asm_p2ds).  The atomic form was never the cause, only the register allocation it led
+   to.  This check flags the pattern in any kernel of the shipped library.
+3. The message aggregation's LDS atomics stay in the flat form every GPU run since round 4 validated (the ds_add_f32
+   form is correct but led the compiler into the copy placement of item 2 in that kernel).
    A run of 8 or more consecutive ds_add_f32 is that aggregation; the shift sums (dxacc) issue at most 2 D per site.
 """
 import os
@@ -23,6 +30,7 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "tools"))
+import isa_exec_copies as XC  # noqa: E402
 import isa_hazards as IH  # noqa: E402
 import kernel_resources as KR  # noqa: E402
 
@@ -59,6 +67,15 @@ def test_no_inline_asm_hazards(disassembly):
     msg = [f"{k}: {d} wait states (need {IH.NEED[k]}): line {a.line} {a.text} -> line {b.line} {b.text}"
            for k, a, b, d in found[:10]]
     assert not found, "\n".join(msg)
+
+
+def test_no_vector_writes_under_zero_exec():
+    found = []
+    fns = XC.functions(KR.LIB)
+    assert len(fns) > 20, "expected the library's kernels"
+    for fn, insts in fns.items():
+        found += [(fn, hex(a), w, r) for a, w, r in XC.check(insts)]
+    assert not found, found[:5]
 
 
 def test_aggregation_atomics_are_flat(disassembly):

@@ -1,6 +1,8 @@
 """Diagnostic: the tangent vf_kernel (ecnf_vf_jvp) of the (128, 2, 3) shape against the fp64 oracle, per molecule, over
 batch sizes, tangent counts, padded (units (48, 80), H = 40) and unpadded (units (128, 128), H = 64) networks, with
-repeats to expose run-to-run differences.  Library: ECNF_LIB (default: the product).  Prints one line per case."""
+repeats to expose run-to-run differences.  Library: ECNF_LIB (default: the product).  Prints one line per case.
+--poison HEX[:MODE]: before every launch, fill every VGPR / AGPR and the LDS of every SIMD with the 32-bit pattern HEX
+(tools/diag/poison.hip, built as tools/diag/libpoison.so) to expose reads of never-written registers or LDS (MODE 1: LDS only, 2: registers only, 3: both, the default)."""
 import ctypes
 import os
 import sys
@@ -15,6 +17,12 @@ from oracle import ecnf_oracle as O  # noqa: E402
 
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 3
 first = "--first" in sys.argv   # one launch (padded network, B = 1, one tangent), then exit: 1 if it is wrong
+poison = None
+if "--poison" in sys.argv:
+    spec = sys.argv[sys.argv.index("--poison") + 1].split(":")
+    bits, pmode = int(spec[0], 16), int(spec[1]) if len(spec) > 1 else 3
+    plib = ctypes.CDLL(os.path.join(ROOT, "tools", "diag", "libpoison.so"))
+    poison = lambda: plib.poison_launch(ctypes.c_uint(bits), 4096, pmode)  # noqa: E731
 for units, H in (((48, 80), 40), ((128, 128), 64)):
     cnf = C.build_cnf(n_frames=7, dim=3, sigma_min=0.01, base_scale=1.0, n_blocks_egnn=2, mlp_units=units,
                       n_invariant_feat_hidden=H, time_embedding_dim=8, n_features=3, device=0)
@@ -32,6 +40,9 @@ for units, H in (((48, 80), 40), ((128, 128), 64)):
             vr, jr = O.egnn_vector_field(p, oc, x0, t, feat, tangents=u, dtype=np.float64)
             outs = []
             for r in range(1 if first else reps):
+                if poison is not None:
+                    torch.cuda.synchronize()
+                    assert poison() == 0
                 v, ju = h.jvp(torch.from_numpy(x0).cuda(), torch.from_numpy(t).cuda(), torch.from_numpy(feat).cuda(),
                               torch.from_numpy(u).cuda())
                 torch.cuda.synchronize()

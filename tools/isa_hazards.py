@@ -27,6 +27,7 @@ REG = re.compile(r"\b([va])(?:(\d+)|\[(\d+):(\d+)\])")
 NEED = {"raw_xdl": 12, "raw_dpp": 2, "raw_exec": 5, "raw_trans": 1, "asm_mfma": 2, "asm_dpp": 2, "asm_rdln": 1,
         "war_xdl": 11}
 TRANS = ("v_exp_", "v_log_", "v_rcp_", "v_rsq_", "v_sqrt_", "v_sin_", "v_cos_")
+THROUGH_CBRANCH = False   # --through-cbranch: conditional branches do not end a window (their fall-through path)
 ASM_OPS = ("v_fmac_f32_dpp", "v_fma_mixlo_f16", "v_fma_mixhi_f16")
 
 
@@ -66,6 +67,8 @@ class Inst:
         self.dpp = "_dpp" in op or " row_" in text or "quad_perm" in text
         self.is_asm = op in ASM_OPS
         self.barrier = op.startswith(("s_cbranch", "s_branch", "s_setpc", "s_swappc", "s_endpgm"))
+        if THROUGH_CBRANCH and op.startswith("s_cbranch"):
+            self.barrier = False   # the fall-through path continues the window
 
 
 def parse(path, func=None):
@@ -143,6 +146,10 @@ def check(insts):
 
 
 def main(argv):
+    global THROUGH_CBRANCH
+    if "--through-cbranch" in argv:
+        THROUGH_CBRANCH = True
+        argv = [a for a in argv if a != "--through-cbranch"]
     path = argv[1]
     func = argv[2] if len(argv) > 2 else None
     found = check(parse(path, func))
