@@ -879,6 +879,29 @@ __device__ __forceinline__ void lds_add(float* p, float v) {
   __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+// m_i += the lane's 16 segment sums of block fb into macc row `row` (the message aggregation's LDS atomics).  The row
+// goes through an empty asm, so the compiler does not precompute (and spill) the 16 lane addresses per block.
+//  * M <= 64 (NF <= 2): an opaque integer row offset -> ds_add_f32 with the 16 offsets in the instruction (ALDP B = 512
+//    PID Hutchinson 24.2 -> 23.4 ms, profiles/round5/ab/ds_vs_flat/);
+//  * M >= 128: an opaque row pointer -> flat_atomic_add_f32 on the LDS aperture.  The ds form is equally fast there
+//    (LJ13 Hutchinson 63.6 ms both), and in the (128, 2, 3) tangent vf_kernel it leads the compiler into a miscompile:
+//    five register copies placed before an EXEC restore where EXEC is 0 (tests/test_isa_hazards.py checks
+//    every shipped kernel for that pattern).
+template <int NF>
+__device__ __forceinline__ void agg_rows(const Lds& s, int row, int kk, int fb, const float (&v)[16]) {
+  if constexpr (NF <= 2) {
+    int mo = row * s.ld_m + 4 * kk;
+    asm volatile("" : "+v"(mo));
+#pragma unroll
+    for (int r16 = 0; r16 < 16; ++r16) lds_add(s.macc + mo + fb * 32 + acc_row(r16, 0), v[r16]);
+  } else {
+    float* mrow = s.macc + row * s.ld_m + 4 * kk;
+    asm volatile("" : "+v"(mrow));
+#pragma unroll
+    for (int r16 = 0; r16 < 16; ++r16) lds_add(mrow + fb * 32 + acc_row(r16, 0), v[r16]);
+  }
+}
+
 // d = w . x (and dT = w . xT) over the lane's NF x 16 feature registers, w an LDS vector in accumulator row order
 // (rows acc_row(r, kk), 16-B reads); the caller adds the other lane half.  Four partial sums, and the weight reads
 // issued one group of 4 ahead behind scheduling fences: the one-accumulator form compiled to 4 NF rounds of
@@ -986,15 +1009,7 @@ __device__ __forceinline__ void edge_tail(const Net& net, const BlockW& bw, cons
           *reinterpret_cast<f32x4*>(agg_dst + fb * 32 + 8 * q + 4 * kk) =
               f32x4{v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
       } else {
-        // per-lane row base through an empty asm: the compiler no longer precomputes (and spills) the 16 lane addresses
-        // per block; the atomics compile to flat_atomic_add_f32 on the LDS aperture.  (The same sum through an opaque
-        // integer offset compiles to ds_add_f32 — correct in itself — but in the (128, 2, 3) tangent vf_kernel that
-        // form's register allocation hit a compiler miscompile: copies placed before an EXEC restore where EXEC is 0,
-        // DESIGN 5.4, checked on every kernel by tests/test_isa_hazards.py.  The flat form is the validated one.)
-        float* mrow = s.macc + rr * s.ld_m + 4 * kk;
-        asm volatile("" : "+v"(mrow));
-#pragma unroll
-        for (int r16 = 0; r16 < 16; ++r16) lds_add(mrow + fb * 32 + acc_row(r16, 0), v[r16]);
+        agg_rows<NF>(s, rr, kk, fb, v);
       }
     }
     if constexpr (NT) {
@@ -1002,10 +1017,7 @@ __device__ __forceinline__ void edge_tail(const Net& net, const BlockW& bw, cons
       for (int r16 = 0; r16 < 16; ++r16) v[r16] = gT * m[fb][r16] + g * mT[fb][r16];
       sc.sum_many<16>(v);
       if (writer) {
-        float* mrow = s.macc + (RP + rr) * s.ld_m + 4 * kk;
-        asm volatile("" : "+v"(mrow));
-#pragma unroll
-        for (int r16 = 0; r16 < 16; ++r16) lds_add(mrow + fb * 32 + acc_row(r16, 0), v[r16]);
+        agg_rows<NF>(s, RP + rr, kk, fb, v);
       }
     }
   }
