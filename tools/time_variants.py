@@ -1,6 +1,6 @@
 """A/B timing of tools/libt_*.so (tools/build_timing.sh): integrate launches of one workload (default LJ13 B=1024
 Euler NFE=100; TV_CASE=aldp_sample / aldp_hutch / lj13_hutch select ALDP B=512 PID sample, ALDP B=512 PID
-Hutchinson log_prob, LJ13 B=1024 Euler Hutchinson, qm9: QM9 B=2048 Euler NFE=20 sample), each library in its own subprocess, ROUNDS interleaved rounds
+Hutchinson log_prob, LJ13 B=1024 Euler Hutchinson, qm9: QM9 B=2048 Euler NFE=20 sample, qm9_hutch: QM9 B=512 Euler NFE=20 Hutchinson), each library in its own subprocess, ROUNDS interleaved rounds
 (A B C A B C ...) so clock drift hits all alike.  Prints the median ms per launch of each library."""
 import glob
 import json
@@ -16,7 +16,8 @@ from ecnf_amd import CONFIGS, init_params
 from ecnf_amd.engine import EcnfHandle, SolveOptions
 from ecnf_amd import _lib
 case = os.environ.get("TV_CASE", "lj13")
-name, B = ("aldp", 512) if case.startswith("aldp") else ("qm9", 2048) if case.startswith("qm9") else ("lj13", 1024)
+name, B = ("aldp", 512) if case.startswith("aldp") else \
+    ("qm9", 512 if case.endswith("hutch") else 2048) if case.startswith("qm9") else ("lj13", 1024)
 cfg = CONFIGS[name]
 h = EcnfHandle(cfg, init_params(cfg, 0), 0)
 z = torch.randn((B, cfg.event_dim), device="cuda", generator=torch.Generator("cuda").manual_seed(0))
