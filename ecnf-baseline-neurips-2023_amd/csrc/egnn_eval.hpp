@@ -881,15 +881,16 @@ __device__ __forceinline__ void lds_add(float* p, float v) {
 
 // m_i += the lane's 16 segment sums of block fb into macc row `row` (the message aggregation's LDS atomics).  The row
 // goes through an empty asm, so the compiler does not precompute (and spill) the 16 lane addresses per block.
-//  * M <= 64 (NF <= 2): an opaque integer row offset -> ds_add_f32 with the 16 offsets in the instruction (ALDP B = 512
-//    PID Hutchinson 24.2 -> 23.4 ms, profiles/round5/ab/ds_vs_flat/);
-//  * M >= 128: an opaque row pointer -> flat_atomic_add_f32 on the LDS aperture.  The ds form is equally fast there
-//    (LJ13 Hutchinson 63.6 ms both), and in the (128, 2, 3) tangent vf_kernel it leads the compiler into a miscompile:
-//    five register copies placed before an EXEC restore where EXEC is 0 (tests/test_isa_hazards.py checks
-//    every shipped kernel for that pattern).
+//  * M = 64 and 256 (NF 2, 8): an opaque integer row offset -> ds_add_f32 with the 16 offsets in the instruction
+//    (interleaved A/B, profiles/round5/ab/ds_vs_flat/: ALDP B = 512 PID Hutchinson 24.2 -> 23.4 ms, QM9 B = 512
+//    Euler-20 Hutchinson 297.5 -> 296.3 ms, QM9 B = 2048 Euler-20 sample 438.6 -> 435.7 ms);
+//  * M = 128 (NF 4): an opaque row pointer -> flat_atomic_add_f32 on the LDS aperture.  The ds form is equally fast
+//    there (LJ13 Hutchinson 63.6 ms both), and in the (128, 2, 3) tangent vf_kernel it leads the compiler into a
+//    miscompile: five register copies placed before an EXEC restore where EXEC is 0 (DESIGN 5.4;
+//    tests/test_isa_hazards.py checks every shipped kernel for that pattern).
 template <int NF>
 __device__ __forceinline__ void agg_rows(const Lds& s, int row, int kk, int fb, const float (&v)[16]) {
-  if constexpr (NF <= 2) {
+  if constexpr (NF != 4) {
     int mo = row * s.ld_m + 4 * kk;
     asm volatile("" : "+v"(mo));
 #pragma unroll
