@@ -14,10 +14,11 @@
    every case correct (tools/diag/asm_swap.py asm_ds_fix); and the same ds_add_f32 atomics swapped into the passing
    build's schedule are correct (asm_p2ds).  The atomic form was never the cause, only the register allocation it led
    to.  This check flags the pattern in any kernel of the shipped library.
-3. The message aggregation's LDS atomics are ds_add_f32 with the row offsets in the instruction (round 5: the form
-   is correct, item 2 was the fault, and it is faster on the M = 64 tangent kernels than the flat_atomic_add_f32
-   form the product used in rounds 4-5).  A run of 16 consecutive ds_add_f32 is that aggregation; the shift sums
-   (dxacc) issue at most 2 D per site.
+3. The message aggregation's LDS atomics are ds_add_f32 with the row offsets in the instruction at M = 64 and 256
+   (round 5: the form is correct, item 2 was the fault, and it is faster there than the flat_atomic_add_f32 form the
+   product used in rounds 4-5; M = 128 stays flat, equally fast, since the ds form hits item 2's miscompile in one of
+   its kernels).  A run of 16 consecutive ds_add_f32 is that aggregation; the shift sums (dxacc) issue at most 2 D
+   per site.
 """
 import os
 import re
