@@ -119,3 +119,19 @@ def test_integrate_kernels_never_touch_scratch(disassembly):
             if split and re.search(r"\bscratch_(load|store)" if team else r"\b(scratch_(load|store)|buffer_store)", line):
                 bad[fn] = bad.get(fn, 0) + 1
     assert not bad, bad
+
+
+def test_exec_copy_checker_known_answers():
+    """tools/isa_exec_copies.check on hand-written blocks: the failing build's pattern (copies ahead of the EXEC restore
+    in a block that s_cbranch_execz enters) is flagged; lane writes, and copies after the restore, are not"""
+    def prog(block):
+        # 0x0: s_and_saveexec; 0x4: s_cbranch_execz -> 0xc (offset 1 dword past the next instruction); 0x8: a VALU
+        head = [(0x0, "s_and_saveexec_b64 s[4:5], vcc"), (0x4, "s_cbranch_execz 1"), (0x8, "v_add_f32_e32 v1, v2, v3")]
+        return head + [(0xc + 4 * k, t) for k, t in enumerate(block)]
+
+    bad = prog(["v_accvgpr_write_b32 a26, v23", "s_or_b64 exec, exec, s[4:5]", "v_accvgpr_read_b32 v23, a26"])
+    found = XC.check(bad)
+    assert len(found) == 1 and found[0][1] == ["v_accvgpr_write_b32 a26, v23"]
+    assert not XC.check(prog(["s_or_b64 exec, exec, s[4:5]", "v_accvgpr_write_b32 a26, v23"]))
+    assert not XC.check(prog(["v_writelane_b32 v253, s3, 0", "s_or_b64 exec, exec, s[4:5]"]))
+    assert not XC.check(prog(["s_nop 0", "s_or_b64 exec, exec, s[4:5]"]))
