@@ -122,16 +122,40 @@ def test_integrate_kernels_never_touch_scratch(disassembly):
 
 
 def test_exec_copy_checker_known_answers():
-    """tools/isa_exec_copies.check on hand-written blocks: the failing build's pattern (copies ahead of the EXEC restore
-    in a block that s_cbranch_execz enters) is flagged; lane writes, and copies after the restore, are not"""
-    def prog(block):
-        # 0x0: s_and_saveexec; 0x4: s_cbranch_execz -> 0xc (offset 1 dword past the next instruction); 0x8: a VALU
-        head = [(0x0, "s_and_saveexec_b64 s[4:5], vcc"), (0x4, "s_cbranch_execz 1"), (0x8, "v_add_f32_e32 v1, v2, v3")]
+    """tools/isa_exec_copies.check on hand-written blocks.  Flagged: vector writes ahead of the first EXEC write of a
+    block entered only with EXEC = 0, for every EXEC-write idiom (s_or_b64 with exec as either source, s_mov_b64 exec,
+    the saveexec family, v_cmpx), however far down the block it sits, and for both zero-EXEC entries (s_cbranch_execz,
+    and the not-taken fall-through of s_cbranch_execnz that exits a divergent loop).  Not flagged: lane writes,
+    writes after the EXEC write, and blocks also entered with live lanes (a plain fall-through or another branch)."""
+    def prog(block, guard="s_cbranch_execz 1"):
+        # 0x0: s_and_saveexec; 0x4: the guard branch -> 0xc; 0x8: s_endpgm (so 0xc has no fall-through)
+        head = [(0x0, "s_and_saveexec_b64 s[4:5], vcc"), (0x4, guard), (0x8, "s_endpgm")]
         return head + [(0xc + 4 * k, t) for k, t in enumerate(block)]
 
-    bad = prog(["v_accvgpr_write_b32 a26, v23", "s_or_b64 exec, exec, s[4:5]", "v_accvgpr_read_b32 v23, a26"])
-    found = XC.check(bad)
-    assert len(found) == 1 and found[0][1] == ["v_accvgpr_write_b32 a26, v23"]
-    assert not XC.check(prog(["s_or_b64 exec, exec, s[4:5]", "v_accvgpr_write_b32 a26, v23"]))
+    copy = "v_accvgpr_write_b32 a26, v23"
+    restores = ["s_or_b64 exec, exec, s[4:5]", "s_or_b64 exec, s[4:5], exec", "s_mov_b64 exec, s[4:5]",
+                "s_or_saveexec_b64 s[6:7], s[4:5]", "s_xor_b64 exec, exec, s[4:5]", "s_and_saveexec_b64 s[6:7], vcc",
+                "v_cmpx_gt_f32_e32 vcc, 0, v1"]
+    for r in restores:
+        found = XC.check(prog([copy, r, "v_accvgpr_read_b32 v23, a26"]))
+        assert len(found) == 1 and found[0][1] == [copy] and found[0][2] == r and found[0][3] == "execz", (r, found)
+    # the whole block is scanned (the round-5 checker stopped after 64 instructions)
+    long_block = [copy] + ["s_nop 0"] * 200 + ["v_mov_b32_e32 v1, v2", restores[2]]
+    found = XC.check(prog(long_block))
+    assert len(found) == 1 and found[0][1] == [copy, "v_mov_b32_e32 v1, v2"]
+    # a block with no EXEC write before its end is scanned to its terminator
+    assert XC.check(prog([copy, "s_endpgm"]))[0][2] == "s_endpgm"
+    # loop exit: the fall-through of a not-taken s_cbranch_execnz (the last iteration cleared EXEC)
+    loop = [(0x0, "v_add_f32_e32 v1, v2, v3"), (0x4, "s_andn2_b64 exec, exec, vcc"), (0x8, "s_cbranch_execnz 65533"),
+            (0xc, copy), (0x10, "s_or_b64 exec, exec, s[4:5]")]
+    found = XC.check(loop)
+    assert len(found) == 1 and found[0][0] == 0xc and found[0][3] == "execnz-fallthrough"
+    # not flagged
+    assert not XC.check(prog(["s_or_b64 exec, exec, s[4:5]", copy]))
     assert not XC.check(prog(["v_writelane_b32 v253, s3, 0", "s_or_b64 exec, exec, s[4:5]"]))
     assert not XC.check(prog(["s_nop 0", "s_or_b64 exec, exec, s[4:5]"]))
+    live_ft = [(0x0, "s_and_saveexec_b64 s[4:5], vcc"), (0x4, "s_cbranch_execz 0"), (0x8, copy),
+               (0xc, "s_or_b64 exec, exec, s[4:5]")]
+    assert not XC.check(live_ft)   # also entered by the fall-through of the execz guard (live lanes)
+    both = prog([copy, "s_or_b64 exec, exec, s[4:5]"]) + [(0x14, "s_cbranch_vccnz 65533")]
+    assert not XC.check(both)      # also the target of a branch on VCC (live lanes)
