@@ -203,10 +203,13 @@ def cpu_model() -> str:
     return "unknown"
 
 
-def cpu_baseline(cfg_name: str, n_mol: int, n_mol_1t: int, nfe: int, threads: int):
-    """The torch-CPU fp32 batched restatement (oracle/torch_ref.py, the batched-GEMM structure XLA builds from
-    vmap) of the same Euler NFE-step sample, timed on `n_mol` molecules with `threads` threads and on `n_mol_1t`
-    molecules with one thread.  Returns (rate_all, secs_all, rate_1t, secs_1t)."""
+def cpu_baseline_child(cfg_name: str, n_mol: int, n_mol_1t: int, nfe: int, threads: int, repeats: int) -> dict:
+    """(runs in a CPU-only child process, see cpu_baseline) the torch-CPU fp32 batched restatement (oracle/torch_ref.py,
+    the batched-GEMM structure XLA builds from vmap) of the same Euler NFE-step sample (torch_ref.sample_euler's time
+    grid) on `n_mol` molecules with `threads` threads and on `n_mol_1t` with one thread.  Every Euler step is timed
+    on its own: the value is molecules / (NFE x the median step time) over the `repeats` x NFE steps, which a transient
+    stall of the host (a slow first solve, another tenant) does not move; the whole-solve rate and the spread of the
+    step times (10th-90th percentile / median) are reported beside it."""
     import numpy as np
     import torch
     from oracle import ecnf_oracle as O
@@ -215,21 +218,48 @@ def cpu_baseline(cfg_name: str, n_mol: int, n_mol_1t: int, nfe: int, threads: in
     P = R.to_torch(O.init_params(oc, 0))
     rng = np.random.default_rng(0)
     z = rng.standard_normal((max(n_mol, n_mol_1t), oc.n_nodes * oc.dim)).astype(np.float32)
-    x0 = torch.from_numpy(O.base_sample(z, oc))
-    feat = torch.zeros((x0.shape[0], oc.n_nodes), dtype=torch.int32)
-    prev = torch.get_num_threads()
-    out = []
-    try:
-        for th, n in ((threads, n_mol), (1, n_mol_1t)):
-            torch.set_num_threads(th)
-            R.sample_euler(P, oc, x0[:2], feat[:2], 2)     # warm-up
-            t0 = time.perf_counter()
-            R.sample_euler(P, oc, x0[:n], feat[:n], nfe)
-            dt = time.perf_counter() - t0
-            out += [n / dt, dt]
-    finally:
-        torch.set_num_threads(prev)
-    return tuple(out)
+    x_all = torch.from_numpy(O.base_sample(z, oc))
+    feat_all = torch.zeros((x_all.shape[0], oc.n_nodes), dtype=torch.int32)
+
+    def solve(n, steps):
+        x, feat, dt, tau, ts = x_all[:n].clone(), feat_all[:n], np.float32(1.0 / nfe), np.float32(0.0), []
+        with torch.no_grad():
+            while tau < 1.0 and len(ts) < steps:
+                tn = np.float32(tau + dt)
+                tn = np.float32(1.0) if tn > np.float32(1.0) - np.float32(1e-6) else tn
+                t0 = time.perf_counter()
+                v = R.vector_field(P, oc, x, torch.full((n,), float(tau), dtype=x.dtype), feat)
+                x = x + float(np.float32(tn - tau)) * v
+                ts.append(time.perf_counter() - t0)
+                tau = tn
+        return ts
+
+    out = {}
+    for key, th, n in (("all", threads, n_mol), ("one", 1, n_mol_1t)):
+        torch.set_num_threads(th)
+        solve(n, 5)                                              # warm-up at the timed batch shape
+        steps = []
+        for _ in range(repeats):
+            steps += solve(n, nfe)
+        med = float(np.median(steps))
+        p10, p90 = np.percentile(steps, [10, 90])
+        out[key] = {"median": n / (nfe * med), "whole_solve": n * repeats / sum(steps),
+                    "spread": float((p90 - p10) / med), "seconds": sum(steps), "threads": torch.get_num_threads(),
+                    "molecules": n, "steps_timed": len(steps)}
+    return out
+
+
+def cpu_baseline(cfg_name: str, n_mol: int, n_mol_1t: int, nfe: int, threads: int, repeats: int):
+    """The CPU baseline, timed in a child process that never touches the GPU, with its OpenMP threads bound one per
+    core of this process's affinity set (OMP_PROC_BIND=close, OMP_PLACES=cores, OMP_NUM_THREADS=threads) so the
+    threads do not migrate; the median of `repeats` timed solves is the reported value and their spread is stated."""
+    env = dict(os.environ, OMP_NUM_THREADS=str(threads), OMP_PROC_BIND="close", OMP_PLACES="cores")
+    cmd = [sys.executable, os.path.abspath(__file__), "--cpu-child",
+           json.dumps([cfg_name, n_mol, n_mol_1t, nfe, threads, repeats])]
+    r = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=600)
+    if r.returncode != 0:
+        raise RuntimeError(f"cpu baseline child failed: {r.stderr[-800:]}")
+    return json.loads(r.stdout.strip().splitlines()[-1])
 
 
 def _free_port() -> int:
@@ -264,8 +294,10 @@ def main():
     ap.add_argument("--train-batch", type=int, default=64, help="training batch (lj13.yaml: 64)")
     ap.add_argument("--ref-latency-samples", type=int, default=10,
                     help="calls of the reference's single-molecule QM9 sampling-time script (first = warm-up; 0 = skip)")
-    ap.add_argument("--cpu-molecules", type=int, default=256, help="bounded CPU-baseline sample (0 = skip)")
-    ap.add_argument("--cpu-molecules-1t", type=int, default=48, help="bounded 1-thread CPU-baseline sample")
+    ap.add_argument("--cpu-molecules", type=int, default=128, help="bounded CPU-baseline sample (0 = skip)")
+    ap.add_argument("--cpu-molecules-1t", type=int, default=24, help="bounded 1-thread CPU-baseline sample")
+    ap.add_argument("--cpu-repeats", type=int, default=1, help="timed CPU-baseline solves (median step time reported)")
+    ap.add_argument("--cpu-child", default="", help=argparse.SUPPRESS)
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "0") or 0))
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL over xGMI) or gloo (multi-rank rehearsal)")
     ap.add_argument("--seed", type=int, default=1234)
@@ -275,6 +307,10 @@ def main():
                          "(default: on at one rank, off over several)")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
+
+    if args.cpu_child:   # the CPU baseline's child process (cpu_baseline): no GPU is touched
+        print(json.dumps(cpu_baseline_child(*json.loads(args.cpu_child))), flush=True)
+        return
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(launch_ranks(args.gpus))
@@ -402,13 +438,18 @@ def main():
             log_w = log_p - log_q
             # reverse ESS of model samples (eval_batch_free_fn, setup_training.py:166-185); the forward ESS needs
             # samples of the TARGET (evaluation.py:10-22, on the test set: ecnf_amd.evaluation), not model samples
-            _, rev = D.ess_from_device(log_w)         # RCCL: one MAX + one SUM all-reduce
+            _, rev = D.ess_from_device(log_w)         # one MAX + one SUM all-reduce (RCCL under nccl)
             mean_lq = D.masked_mean(log_q)
             torch.cuda.synchronize(dev)
             barrier()
             t_lp = max_over_ranks(time.perf_counter() - t1)
+        # the backend that actually reduced the ESS / mean statistics: the formed process group's (RCCL for nccl),
+        # or none in a plain one-process run (distributed._allreduce is then the identity)
+        red = dist.get_backend() if dist.is_initialized() else None
+        red = {"nccl": "RCCL", None: "local reductions (one process, no process group)"}.get(red, red)
         logprob = {"workload": f"{args.config} sample_and_log_prob_cnf (Hutchinson, Euler NFE={args.nfe}) + target "
-                               f"log-density + ESS over {'RCCL' if args.dist_backend == 'nccl' else args.dist_backend}",
+                               f"log-density + ESS, {red}",
+                   "reduced_by": red,
                    "molecules_per_s": G / t_lp, "ms": t_lp * 1e3,
                    # the divergence kernel alone (HIP events on its stream): primal + one tangent per evaluation
                    "kernel_ms": ek0.elapsed_time(ek1),
@@ -507,13 +548,18 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and args.cpu_molecules > 0:
         threads = args.cpu_threads or len(os.sched_getaffinity(0))
-        r_all, s_all, r_1, s_1 = cpu_baseline(args.config, args.cpu_molecules, args.cpu_molecules_1t, args.nfe,
-                                              threads)
-        cpu = {"value": r_all, "unit": "molecules/s", "cores": threads, "kind": "port",
-               "value_1_thread": r_1, "cpu_model": cpu_model(),
-               "sample": f"{args.cpu_molecules} {args.config} molecules x {args.nfe} Euler steps on {threads} threads "
-                         f"({s_all:.1f} s) and {args.cpu_molecules_1t} on 1 thread ({s_1:.1f} s); torch-CPU fp32 "
-                         f"batched restatement (oracle/torch_ref.py)"}
+        cb = cpu_baseline(args.config, args.cpu_molecules, args.cpu_molecules_1t, args.nfe, threads,
+                          max(1, args.cpu_repeats))
+        a1, o1 = cb["all"], cb["one"]
+        cpu = {"value": a1["median"], "unit": "molecules/s", "cores": a1["threads"], "kind": "port",
+               "whole_solve_value": a1["whole_solve"], "step_time_spread_p10_p90": a1["spread"],
+               "value_1_thread": o1["median"], "whole_solve_value_1_thread": o1["whole_solve"],
+               "cpu_model": cpu_model(),
+               "sample": f"{args.cpu_molecules} {args.config} molecules x {args.nfe} Euler steps "
+                         f"(x{max(1, args.cpu_repeats)}) on {a1['threads']} threads bound to the affinity set's cores "
+                         f"({a1['seconds']:.1f} s) and {args.cpu_molecules_1t} on 1 thread ({o1['seconds']:.1f} s); "
+                         f"value = molecules / (NFE x median step time); torch-CPU fp32 batched restatement "
+                         f"(oracle/torch_ref.py) in a CPU-only child process"}
 
     if rank == 0:
         out = {

@@ -341,7 +341,9 @@ struct ecnf_handle {
   // ecnf_integrate on the handle (ordered across streams by team_ev under team_mu)
   std::atomic<int> team_mode;   // ecnf_set_team: 0 auto, 1 off, G >= 2 forced; read once per solve (team_size)
   int team_cap, team_gcap, team_slot;
-  float* team_buf;
+  // atomic: team_size reads it without team_mu while ecnf_update_params may publish new buffers under it (team_sync
+  // is only read with team_mu held: the G > 1 dispatch in integrate_impl)
+  std::atomic<float*> team_buf{nullptr};
   unsigned* team_sync;  // [team_cap] counters, then [team_cap] timeout flags (one 16-B-padded block, zeroed per launch)
   std::mutex team_mu;
   hipEvent_t team_ev;
@@ -639,7 +641,7 @@ bool cols_fits(const ecnf_handle* h, int NT, int B) {
 int team_size(const ecnf_handle* h, int NT, int B, int* cols, int mode) {
   const ecnf_cfg& c = h->cfg;
   if (cols) *cols = 0;
-  if (NT != 0 || B < 1 || B > h->team_cap || mode == 1 || !h->team_buf ||
+  if (NT != 0 || B < 1 || B > h->team_cap || mode == 1 || !h->team_buf.load() ||
       !team_shape(c.mlp_width, NT, c.mlp_depth, c.dim, h->prec))
     return 1;
   const int tpm = h->net[0].EP / 32;
@@ -679,7 +681,7 @@ hipError_t dispatch_integrate(const ecnf_handle* h, int NT, const SolveP& sp_in,
     sp.team.G = G;
     sp.team.cols = cols;
     sp.team.slot = h->team_slot;
-    sp.team.buf = h->team_buf;
+    sp.team.buf = h->team_buf.load();
     sp.team.ctr = h->team_sync;
     sp.team.timeout = reinterpret_cast<int*>(h->team_sync + kTeamCap);
     hipError_t e = hipMemsetAsync(h->team_sync, 0, kTeamSyncBytes, stream);
@@ -1147,8 +1149,11 @@ int ecnf_create(const ecnf_cfg* cfg, const float* params, size_t n_floats, int d
     h->team_slot = c.n_nodes * M + tpm * M + ((c.n_nodes * c.dim + 3) & ~3);
     const size_t nb = (size_t)h->team_cap * 2 * h->team_gcap * h->team_slot * sizeof(float);
     const bool want = h->split_ok && team_shape(c.mlp_width, 0, c.mlp_depth, c.dim, 0);
-    if (want && (hipMalloc(&h->team_buf, nb) != hipSuccess || hipMalloc(&h->team_sync, kTeamSyncBytes) != hipSuccess)) {
-      if (h->team_buf) hipFree(h->team_buf);
+    float* tb = nullptr;
+    const bool ok_buf = !want || hipMalloc(&tb, nb) == hipSuccess;
+    h->team_buf.store(tb);
+    if (want && (!ok_buf || hipMalloc(&h->team_sync, kTeamSyncBytes) != hipSuccess)) {
+      if (tb) hipFree(tb);
       hipFree(dbuf);
       delete h;
       return fail(ECNF_E_HIP, "team-mode exchange buffers: out of device memory");
@@ -1183,10 +1188,10 @@ int ecnf_update_params(ecnf_handle* h, const float* params, int32_t on_device) {
   }
   h->split_ok = t->split_ok;
   if (!h->split_ok) h->prec = ECNF_PREC_FP32;
-  if (!h->team_buf && t->team_buf) {   // the new weights admit the split team kernels the old ones did not
+  if (!h->team_buf.load() && t->team_buf.load()) {   // the new weights admit the split team kernels the old ones did not
     std::lock_guard<std::mutex> tl(h->team_mu);
-    std::swap(h->team_buf, t->team_buf);
     std::swap(h->team_sync, t->team_sync);
+    t->team_buf.store(h->team_buf.exchange(t->team_buf.load()));   // team_sync first: team_size keys on team_buf
   }
   return ecnf_destroy(t);
 }
@@ -1198,7 +1203,7 @@ int ecnf_destroy(ecnf_handle* h) {
   HIP_TRY(hipFree(h->dbuf));
   if (h->arena) HIP_TRY(hipFree(h->arena));
   if (h->arena_ev) HIP_TRY(hipEventDestroy(h->arena_ev));
-  if (h->team_buf) HIP_TRY(hipFree(h->team_buf));
+  if (h->team_buf.load()) HIP_TRY(hipFree(h->team_buf.load()));
   if (h->team_sync) HIP_TRY(hipFree(h->team_sync));
   if (h->team_ev) HIP_TRY(hipEventDestroy(h->team_ev));
   delete h;
@@ -1265,6 +1270,30 @@ int ecnf_integrate_workspace_size(ecnf_handle* h, const ecnf_solve_opts* o, int3
   if (!h || !o || !bytes) return fail(ECNF_E_INVALID, "NULL argument");
   if (batch < 0) return fail(ECNF_E_INVALID, "batch < 0");
   *bytes = ((exact_sparse(h, o->divergence) ? pcache_floats(h, batch) : 0) + sched_floats(h, o, batch)) * sizeof(float);
+  return ECNF_OK;
+}
+
+int ecnf_integrate_plan(ecnf_handle* h, const ecnf_solve_opts* o, int32_t batch, int32_t* workgroups,
+                        int32_t* launches) {
+  if (!h || !o || !workgroups || !launches) return fail(ECNF_E_INVALID, "NULL argument");
+  if (batch < 1) return fail(ECNF_E_INVALID, "batch < 1");
+  if (o->divergence < ECNF_DIV_NONE || o->divergence > ECNF_DIV_EXACT) return fail(ECNF_E_INVALID, "unknown divergence");
+  const int NT = o->divergence == ECNF_DIV_NONE ? 0 : 1, ix = 2 * h->prec + NT;
+  if (NT && h->net[ix].MPW == 0) return fail(ECNF_E_UNSUPPORTED, no_tangent_msg(h->cfg, h->prec));
+  const bool adaptive = !(o->dt0 > 0.f);
+  const int G = team_size(h, NT, batch, nullptr, h->team_mode.load());
+  if (G > 1) {
+    *workgroups = batch * G;
+    *launches = 1;
+    return ECNF_OK;
+  }
+  // dispatch_integrate's decision, with a workspace of ecnf_integrate_workspace_size bytes
+  size_t lds = 0;
+  const Net net = net_for_batch(h, ix, batch, &lds, adaptive);
+  const int grid = (batch + net.MPW - 1) / net.MPW;
+  *workgroups = grid;
+  *launches = (sched_floats(h, o, batch) > 0 && adaptive && grid > h->ncu &&
+               chunkable(h->cfg.mlp_width / 32, NT, h->prec)) ? 2 : 1;
   return ECNF_OK;
 }
 

@@ -235,8 +235,9 @@ __global__ __launch_bounds__((kernel_threads<NF, NT, P, COLS>())) __attribute__(
   ECNF_DCHECK((int)(s.tail - smem) + solver_lds_floats(MPW, ND) <= net.lds_floats, 0);
   ECNF_DCHECK(nmol >= 1 && nmol <= MPW, 5);
 
-  // zero the eval scratch (aggregates must start at +0; padding rows stay finite)
-  for (int i = tid; i < (int)(s.tail - smem); i += kThreads) smem[i] = 0.f;
+  // zero the eval scratch and the solver state (aggregates must start at +0; padding rows and the solver slots of
+  // padding molecules stay finite: a resumed launch loads kx[0] / kl of the occupied slots only)
+  for (int i = tid; i < (int)(s.tail - smem) + solver_lds_floats(MPW, ND); i += kThreads) smem[i] = 0.f;
   __syncthreads();
   for (int i = tid; i < MPW * ND; i += kThreads) {
     const int m = i / ND;

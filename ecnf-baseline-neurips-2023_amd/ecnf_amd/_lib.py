@@ -27,7 +27,7 @@ EXPORTED_SYMBOLS = (
     "ecnf_set_precision", "ecnf_get_precision", "ecnf_trainer_create", "ecnf_trainer_destroy", "ecnf_fm_loss_grad",
     "ecnf_adam_update", "ecnf_update_params", "ecnf_integrate_workspace_size", "ecnf_integrate_ws",
     "ecnf_reserve_workspace", "ecnf_set_exact_form", "ecnf_struct_layout", "ecnf_trainer_set_reduction_arena",
-    "ecnf_set_team", "ecnf_team_workgroups",
+    "ecnf_set_team", "ecnf_team_workgroups", "ecnf_integrate_plan",
 )
 
 TARGET_LJ, TARGET_DW = 0, 1
@@ -157,6 +157,8 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
         "ecnf_set_exact_form": ([P, I32], ctypes.c_int),
         "ecnf_set_team": ([P, I32], ctypes.c_int),
         "ecnf_team_workgroups": ([P, I32, I32, ctypes.POINTER(I32)], ctypes.c_int),
+        "ecnf_integrate_plan": ([P, ctypes.POINTER(EcnfSolveOpts), I32, ctypes.POINTER(I32), ctypes.POINTER(I32)],
+                                ctypes.c_int),
         "ecnf_struct_layout": ([I32, ctypes.POINTER(SZ), I32], ctypes.c_int),
     }
     for name, (argtypes, restype) in sig.items():

@@ -307,6 +307,15 @@ class EcnfHandle:
         _lib.check(self.lib.ecnf_team_workgroups(self._h, int(with_tangent), int(batch), ctypes.byref(g)))
         return g.value
 
+    def integrate_plan(self, batch: int, t0: float, t1: float, opts: "SolveOptions",
+                       divergence: int = _lib.DIV_NONE) -> Tuple[int, int]:
+        """(workgroups of the first launch, launches) of a solve given a workspace of ecnf_integrate_workspace_size
+        bytes (ecnf_integrate_plan; 2 launches: the chunked, re-dealt adaptive solve)."""
+        o = opts.to_c(t0, t1, divergence)
+        wg, nl = ctypes.c_int32(), ctypes.c_int32()
+        _lib.check(self.lib.ecnf_integrate_plan(self._h, ctypes.byref(o), int(batch), ctypes.byref(wg), ctypes.byref(nl)))
+        return wg.value, nl.value
+
     def base_sample(self, z) -> torch.Tensor:
         z = self._f32(z, (self.cfg.event_dim,), "z")
         x0 = torch.empty_like(z)

@@ -146,6 +146,11 @@ int ecnf_integrate_ws(ecnf_handle* h, const ecnf_solve_opts* opts, const float* 
                       const float* eps, float* y1, float* dlogp, int32_t* nfe, int32_t* status, int32_t batch,
                       void* workspace, size_t workspace_bytes, void* stream);
 int ecnf_reserve_workspace(ecnf_handle* h, size_t bytes);
+/* Diagnostic: how a solve with these options and batch is launched when given a workspace of
+ * ecnf_integrate_workspace_size bytes -- the workgroups of its (first) launch and the number of launches (2: the
+ * chunked, re-dealt adaptive solve above; 1: one launch). */
+int ecnf_integrate_plan(ecnf_handle* h, const ecnf_solve_opts* opts, int32_t batch, int32_t* workgroups,
+                        int32_t* launches);
 
 /* A/B diagnostics of the exact trace (not needed in production; results: SPARSE and DEFAULT are bitwise equal, ALL_DUAL
  * agrees to fp32 rounding):  DEFAULT  sparse blocks 1 and K + the primal cache when a workspace is available;

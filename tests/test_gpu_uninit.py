@@ -68,3 +68,32 @@ def test_results_do_not_depend_on_stale_registers(poison, name, B, precision):
         assert torch.equal(p, q), f"output {k} differs with poisoned registers / LDS"
     assert all(bool(torch.isfinite(p.float()).all()) for p in a[:5])
     h.close()
+
+
+@pytest.mark.timeout(240)
+def test_redealt_adaptive_solve_does_not_depend_on_stale_state(poison):
+    """The re-dealt adaptive solve (two launches, tests/test_gpu_redeal.py): the second launch loads the stored state of
+    its occupied slots only, so the padding slots of its last workgroup (slots past the unfinished count) must start
+    from the kernel's zero fill of the eval AND solver LDS, not from whatever the previous launch or a poison pattern
+    left there.  ALDP B = 1101 PID sample_cnf (several molecules per workgroup; the engine passes a workspace, so the
+    solve is re-dealt, asserted through ecnf_integrate_plan), bitwise equal under a zero and a NaN fill."""
+    cfg = CONFIGS["aldp"]
+    h = EcnfHandle(cfg, init_params(cfg, 0), 0)
+    B = 1101
+    opts = SolveOptions("dopri5", None)
+    wg, launches = h.integrate_plan(B, 0.0, 1.0, opts, _lib.DIV_NONE)
+    assert launches == 2 and wg < B, (wg, launches)   # re-dealt, more than one molecule per workgroup
+    g = torch.Generator("cuda").manual_seed(9)
+    z = torch.randn((B, cfg.event_dim), device="cuda", generator=g)
+    x = h.base_sample(z)
+    feat = (torch.arange(cfg.n_nodes, device="cuda", dtype=torch.int32) % cfg.n_features).expand(B, -1).contiguous()
+    outs = []
+    for bits in (0x00000000, 0x7FC00000):
+        poison(bits)
+        y, _, nfe, st = h.integrate(x, feat, 0.0, 1.0, opts, _lib.DIV_NONE, None, check_status=False)
+        torch.cuda.synchronize()
+        outs.append((y, nfe, st))
+    for p, q in zip(*outs):
+        assert torch.equal(p, q)
+    assert int(outs[0][2].abs().sum()) == 0 and bool(torch.isfinite(outs[0][0]).all())
+    h.close()
