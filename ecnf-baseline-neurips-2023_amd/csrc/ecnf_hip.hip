@@ -198,9 +198,18 @@ __host__ __device__ inline int pow2_at_least(int n) {
 // makespan equals that of the true remaining-NFE order, the rest is the first launch's two rounds of 512 workgroups
 constexpr int kChunkSteps = 8;
 
+// Tail teams (ALDP's tangent kernels, team_shape with NT = 1): the re-dealt launch runs its K longest-estimate slots as
+// teams of kTailG workgroups (egnn_eval.hpp team_exchange; results bitwise the batch path's), an evaluation 1.24 times
+// faster at 2 CUs (tools/team_tangent_probe.py: ALDP 107 us per evaluation alone, G = 2 / 3 / 4: 86 / 85 / 75 us).
+// K = the longest eighth of the unfinished slots, at most kmax (the exchange buffers; at most half the CUs in teams).
+// Chosen by measurement against the alternatives (tools/diag/tail_sim.py, profiles/round6/aldp_tail/): ALDP B = 512
+// PID Hutchinson log_prob from base draws 42.6 -> 37.7 ms (G = 4 with a makespan model choosing K = 26: 39.3 ms; G = 4,
+// K = 32: 39.7 ms); from real frames, whose long solves the 8-step estimate ranks worse, 49.8 -> 50.4 ms.
+constexpr int kTailG = 2;
+
 __global__ __launch_bounds__(kRedealThreads) void redeal_kernel(const float* __restrict__ state, int stride, int ND,
                                                                 int B, float tau1, int* order, int* nslots, float* gkey,
-                                                                int* gidx) {
+                                                                int* gidx, int* nteam, int kmax) {
   __shared__ float lkey[kRedealLds];
   __shared__ int lidx[kRedealLds];
   const int tid = threadIdx.x;
@@ -245,6 +254,9 @@ __global__ __launch_bounds__(kRedealThreads) void redeal_kernel(const float* __r
     if (i + 1 == B || !(key[i + 1] > -INFINITY)) *nslots = i + 1;
   }
   if (tid == 0 && !(key[0] > -INFINITY)) *nslots = 0;
+  if (!nteam) return;
+  __syncthreads();
+  if (tid == 0) *nteam = min(kmax, (*nslots + 7) / 8);
 }
 
 }  // namespace ecnf
@@ -460,7 +472,8 @@ struct HostBlock {
 };
 
 // team mode (team_size): molecules per launch, and the bytes of the counter / timeout block (16-B multiple)
-constexpr int kTeamCap = 32;
+constexpr int kTeamCap = 64;      // molecules with team buffers (forced team mode, the re-dealt solve's tail teams)
+constexpr int kTeamAutoMax = 32;  // auto team mode up to this batch (include/ecnf.h ecnf_set_team)
 constexpr size_t kTeamSyncBytes = 2 * kTeamCap * sizeof(unsigned);
 
 // waves per workgroup of the primal kernels (Geo<NF, 0, P>::NW)
@@ -637,13 +650,17 @@ bool cols_fits(const ecnf_handle* h, int NT, int B) {
   return lds_bytes(c, 0, 0, 1, RP) + (size_t)cols_image_floats(c) * 4 + kStaticLdsBytes <= 160 * 1024;
 }
 
-// mode: the handle's team_mode, read ONCE by the caller (a concurrent ecnf_set_team cannot split one solve's decision)
-int team_size(const ecnf_handle* h, int NT, int B, int* cols, int mode) {
+// mode: the handle's team_mode, read ONCE by the caller (a concurrent ecnf_set_team cannot split one solve's decision).
+// Tangent solves run in team mode only when forced (mode >= 2), for the Hutchinson divergence (the exact trace's
+// sparse blocks are not exchanged) on the tangent team shape (team_shape: ALDP's M = 64 kernel, one molecule per
+// workgroup); the re-dealt adaptive log_prob teams its tail on its own (team_tail).
+int team_size(const ecnf_handle* h, int NT, int B, int* cols, int mode, int div = ECNF_DIV_HUTCHINSON) {
   const ecnf_cfg& c = h->cfg;
   if (cols) *cols = 0;
-  if (NT != 0 || B < 1 || B > h->team_cap || mode == 1 || !h->team_buf.load() ||
+  if (B < 1 || B > (mode >= 2 ? h->team_cap : kTeamAutoMax) || mode == 1 || !h->team_buf.load() ||
       !team_shape(c.mlp_width, NT, c.mlp_depth, c.dim, h->prec))
     return 1;
+  if (NT && (mode < 2 || div != ECNF_DIV_HUTCHINSON)) return 1;
   const int tpm = h->net[0].EP / 32;
   int G;
   if (mode >= 2) {
@@ -658,6 +675,14 @@ int team_size(const ecnf_handle* h, int NT, int B, int* cols, int mode) {
   }
   if (G < 2 || (long)B * G > h->ncu) return 1;
   return G;
+}
+
+// Does a re-dealt solve on this handle run its longest slots as tail teams (redeal_kernel, kTailG)?  Hutchinson solves
+// of a shape with a tangent team kernel (team_shape), one molecule per workgroup, split precision, team buffers present.
+bool tail_teams(const ecnf_handle* h, int NT, int div, int mpw) {
+  const ecnf_cfg& c = h->cfg;
+  return NT == 1 && div == ECNF_DIV_HUTCHINSON && mpw == 1 && h->prec == 0 && h->team_buf.load() &&
+         h->team_mode.load() != 1 && kTailG <= h->team_gcap && team_shape(c.mlp_width, 1, c.mlp_depth, c.dim, 0);
 }
 
 // G, cols: team_size's decision for this solve (G = 1: the batch path)
@@ -680,6 +705,7 @@ hipError_t dispatch_integrate(const ecnf_handle* h, int NT, const SolveP& sp_in,
     net.lds_floats = (int)(lds / 4);
     sp.team.G = G;
     sp.team.cols = cols;
+    sp.team.nteam = nullptr;
     sp.team.slot = h->team_slot;
     sp.team.buf = h->team_buf.load();
     sp.team.ctr = h->team_sync;
@@ -720,8 +746,13 @@ hipError_t dispatch_integrate(const ecnf_handle* h, int NT, const SolveP& sp_in,
   s1.chunk_steps = kChunkSteps;
   hipError_t e = launch(s1);
   if (e != hipSuccess) return e;
+  // tail teams (kTailG workgroups for the longest slots) where the shape has a tangent team kernel and the batch runs
+  // one molecule per workgroup; the caller holds team_mu (integrate_impl) and the team buffers are this solve's
+  const bool tail = tail_teams(h, NT, sp.div, net.MPW);
+  const int kmax = tail ? std::min(h->team_cap, h->ncu / (2 * kTailG)) : 0;
+  int* nteam = tail ? nslots + 1 : nullptr;
   hipLaunchKernelGGL(redeal_kernel, dim3(1), dim3(kRedealThreads), 0, stream, sched, stride, ND, B, sp.tau1, order,
-                     nslots, gkey, gidx);
+                     nslots, gkey, gidx, nteam, kmax);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   SolveP s2 = sp;
@@ -730,6 +761,18 @@ hipError_t dispatch_integrate(const ecnf_handle* h, int NT, const SolveP& sp_in,
   s2.resume = 1;
   s2.order = order;
   s2.nslots = nslots;
+  if (tail) {
+    s2.team.G = kTailG;
+    s2.team.cols = 0;
+    s2.team.slot = h->team_slot;
+    s2.team.buf = h->team_buf.load();
+    s2.team.ctr = h->team_sync;
+    s2.team.timeout = reinterpret_cast<int*>(h->team_sync + kTeamCap);
+    s2.team.nteam = nteam;
+    s2.team.nteam_max = kmax;
+    e = hipMemsetAsync(h->team_sync, 0, kTeamSyncBytes, stream);
+    if (e != hipSuccess) return e;
+  }
   return launch(s2);
 }
 
@@ -1146,9 +1189,11 @@ int ecnf_create(const ecnf_cfg* cfg, const float* params, size_t n_floats, int d
     h->team_cap = kTeamCap;
     // (M = 256: room for the column-split mode's G = tiles per molecule)
     h->team_gcap = c.mlp_width == 256 ? tpm : std::min(tpm, std::max(4, (tpm + primal_waves(c) - 1) / primal_waves(c)));
-    h->team_slot = c.n_nodes * M + tpm * M + ((c.n_nodes * c.dim + 3) & ~3);
+    // (the tangent team kernels also exchange the tangent message and shift rows: egnn_eval.hpp team_exchange)
+    const bool tan_team = team_shape(c.mlp_width, 1, c.mlp_depth, c.dim, 0);
+    h->team_slot = (tan_team ? 2 : 1) * (c.n_nodes * M + ((c.n_nodes * c.dim + 3) & ~3)) + tpm * M;
     const size_t nb = (size_t)h->team_cap * 2 * h->team_gcap * h->team_slot * sizeof(float);
-    const bool want = h->split_ok && team_shape(c.mlp_width, 0, c.mlp_depth, c.dim, 0);
+    const bool want = h->split_ok && (team_shape(c.mlp_width, 0, c.mlp_depth, c.dim, 0) || tan_team);
     float* tb = nullptr;
     const bool ok_buf = !want || hipMalloc(&tb, nb) == hipSuccess;
     h->team_buf.store(tb);
@@ -1281,7 +1326,7 @@ int ecnf_integrate_plan(ecnf_handle* h, const ecnf_solve_opts* o, int32_t batch,
   const int NT = o->divergence == ECNF_DIV_NONE ? 0 : 1, ix = 2 * h->prec + NT;
   if (NT && h->net[ix].MPW == 0) return fail(ECNF_E_UNSUPPORTED, no_tangent_msg(h->cfg, h->prec));
   const bool adaptive = !(o->dt0 > 0.f);
-  const int G = team_size(h, NT, batch, nullptr, h->team_mode.load());
+  const int G = team_size(h, NT, batch, nullptr, h->team_mode.load(), o->divergence);
   if (G > 1) {
     *workgroups = batch * G;
     *launches = 1;
@@ -1327,7 +1372,7 @@ int ecnf_set_team(ecnf_handle* h, int32_t mode) {
 
 int ecnf_team_workgroups(ecnf_handle* h, int32_t with_tangent, int32_t batch, int32_t* G) {
   if (!h || !G) return fail(ECNF_E_INVALID, "NULL argument");
-  *G = team_size(h, with_tangent ? 1 : 0, batch, nullptr, h->team_mode.load());
+  *G = team_size(h, with_tangent ? 1 : 0, batch, nullptr, h->team_mode.load(), ECNF_DIV_HUTCHINSON);
   return ECNF_OK;
 }
 
@@ -1403,7 +1448,7 @@ int integrate_impl(ecnf_handle* h, const ecnf_solve_opts* o, const float* y0, co
   sp.resume = 0;
   // team mode decided once for this solve: one read of the handle's mode (ecnf_set_team may run concurrently)
   int cols = 0;
-  const int G = team_size(h, NT, batch, &cols, h->team_mode.load());
+  const int G = team_size(h, NT, batch, &cols, h->team_mode.load(), o->divergence);
   const size_t need = sp.sparse1 ? pcache_floats(h, batch) : 0;
   const size_t need_s = G == 1 ? sched_floats(h, o, batch) : 0;
   // the arena pointer and size are read under arena_mu, and the lock is held through the dispatch that uses them:
@@ -1422,6 +1467,20 @@ int integrate_impl(ecnf_handle* h, const ecnf_solve_opts* o, const float* y0, co
   // the re-deal scratch follows the pcache region (a workspace too small for both runs the solve in one launch)
   float* sched = need_s && ws && ws_bytes >= (need + need_s) * sizeof(float) ? ws + need : nullptr;
   HIP_TRY(hipSetDevice(h->device));
+  // a re-dealt solve with tail teams uses the handle's team buffers: ordered like the team-mode solves (team_mu, team_ev)
+  std::unique_lock<std::mutex> tlk(h->team_mu, std::defer_lock);
+  if (sched && tail_teams(h, NT, o->divergence, h->net[2 * h->prec + NT].MPW)) {
+    tlk.lock();
+    if (!h->team_ev) HIP_TRY(hipEventCreateWithFlags(&h->team_ev, hipEventDisableTiming));
+    if (h->team_used && h->team_stream != stream) HIP_TRY(hipStreamWaitEvent(stream, h->team_ev, 0));
+  }
+  auto team_done = [&]() -> hipError_t {
+    if (!tlk.owns_lock()) return hipSuccess;
+    const hipError_t e = hipEventRecord(h->team_ev, stream);
+    h->team_used = true;
+    h->team_stream = stream;
+    return e;
+  };
   if ((cached || sched) && arena) {
     // the arena is shared by every ecnf_integrate call on the handle: calls on different streams are ordered
     // through an event (no host synchronisation), and the bookkeeping is guarded for calls from several threads
@@ -1429,6 +1488,7 @@ int integrate_impl(ecnf_handle* h, const ecnf_solve_opts* o, const float* y0, co
     if (!h->arena_ev) HIP_TRY(hipEventCreateWithFlags(&h->arena_ev, hipEventDisableTiming));
     if (h->arena_used && h->arena_stream != stream) HIP_TRY(hipStreamWaitEvent(stream, h->arena_ev, 0));
     HIP_TRY(dispatch_integrate(h, NT, sp, G, cols, y0, feat, eps, y1, dlogp, nfe, status, batch, stream, sched));
+    HIP_TRY(team_done());
     HIP_TRY(hipEventRecord(h->arena_ev, stream));
     h->arena_used = true;
     h->arena_stream = stream;
@@ -1443,6 +1503,7 @@ int integrate_impl(ecnf_handle* h, const ecnf_solve_opts* o, const float* y0, co
     h->team_stream = stream;
   } else {
     HIP_TRY(dispatch_integrate(h, NT, sp, G, cols, y0, feat, eps, y1, dlogp, nfe, status, batch, stream, sched));
+    HIP_TRY(team_done());
   }
   g_err.clear();
   return ECNF_OK;

@@ -219,12 +219,31 @@ __global__ __launch_bounds__((kernel_threads<NF, NT, P, COLS>())) __attribute__(
   const int tid = (int)threadIdx.x, MPW = net.MPW, ND = net.ND, N = net.N;
   const Lds s = carve_lds<NT, Geo<NF, NT, P, BN>::kSplitN, Geo<NF, NT, P, BN>::kNoP>(net, smem);
   const SolverLds st = carve_solver(s.tail, MPW, ND);
-  // team mode: workgroup blockIdx = T G + r is member r of molecule T's team (MPW = 1); only member 0 writes outputs
+  // team mode (MPW = 1; only member 0 writes outputs): the K G workgroups [0, K G) are the members of slots [0, K),
+  // in groups of 8 teams whose members sit 8 (or the last group's team count) blocks apart -- member r of team 8 q + j
+  // is block 8 G q + nl r + j, nl = min(8, K - 8 q) -- so that under the round-robin block -> XCD dispatch a team's
+  // members share one XCD and its L2 (the exchange's write-through stores and loads then stay in that L2;
+  // MI355X_MICROARCH.md: placement is for speed only, the hand-off protocol does not depend on it).  K = B, or
+  // *sp.team.nteam for the re-dealt solve's tail teams, whose other slots run alone from block K G on (G = 1, no
+  // exchange)
   TeamCtx team_ctx;
   constexpr bool team = TEAM;
   team_ctx.p = sp.team;
-  team_ctx.T = team ? (int)blockIdx.x / sp.team.G : 0;
-  team_ctx.r = team ? (int)blockIdx.x - team_ctx.T * sp.team.G : 0;
+  team_ctx.T = 0;
+  team_ctx.r = 0;
+  team_ctx.G = 1;
+  if constexpr (team) {
+    const int G = sp.team.G, b = (int)blockIdx.x;
+    const int K = sp.team.nteam ? *sp.team.nteam : B;
+    if (b < K * G) {
+      const int q = b / (8 * G), nl = min(8, K - 8 * q), rem = b - 8 * G * q;
+      team_ctx.r = rem / nl;
+      team_ctx.T = 8 * q + (rem - team_ctx.r * nl);
+      team_ctx.G = G;
+    } else {
+      team_ctx.T = K + (b - K * G);
+    }
+  }
   const TeamCtx* tm = team ? &team_ctx : nullptr;
   int tepoch = 0;
   const bool writer_wg = team_ctx.r == 0;
@@ -555,8 +574,8 @@ __global__ __launch_bounds__((kernel_threads<NF, NT, P, COLS>())) __attribute__(
   }
   if constexpr (team) {
     // an exchange that timed out (a member not co-resident) leaves this molecule's results undefined
-    if (tid == 0 && __hip_atomic_load((ECNF_GLOBAL int*)(sp.team.timeout + team_ctx.T), __ATOMIC_RELAXED,
-                                      __HIP_MEMORY_SCOPE_AGENT))
+    if (tid == 0 && team_ctx.G > 1 &&
+        __hip_atomic_load((ECNF_GLOBAL int*)(sp.team.timeout + team_ctx.T), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
       st.status[0] = ECNF_E_HIP;
     __syncthreads();
     if (!writer_wg) return;
@@ -623,9 +642,11 @@ __global__ __launch_bounds__((Geo<NF, NT, P>::NTHR)) __attribute__((amdgpu_waves
 }
 
 // shapes with a team-mode kernel (ecnf_hip.hip team_size): the split primal kernels of the BASELINE networks
-// (QM9 M = 256, LJ13 M = 128, ALDP M = 64)
+// (QM9 M = 256, LJ13 M = 128, ALDP M = 64), and ALDP's split tangent kernel (Hutchinson solves: the re-dealt adaptive
+// log_prob's tail teams, redeal_kernel; one molecule per workgroup)
 constexpr bool team_shape(int M, int NT, int L, int D, int P) {
-  return NT == 0 && P == 0 && D == 3 && ((M == 256 && L == 4) || (M == 128 && L == 3) || (M == 64 && L == 2));
+  return P == 0 && D == 3 &&
+         (NT == 0 ? ((M == 256 && L == 4) || (M == 128 && L == 3) || (M == 64 && L == 2)) : (M == 64 && L == 2));
 }
 
 // shapes with a column-split team kernel (egnn_eval.hpp edge_tile_cols): the M = 256 team shape (QM9; 4 waves split
@@ -638,6 +659,17 @@ hipError_t launch_integrate(const Net& net, size_t lds, const SolveP& sp, const 
                             const float* eps, float* y1, float* dlogp, int32_t* nfe, int32_t* status, int B,
                             hipStream_t stream) {
   if constexpr (team_shape(NF * 32, NT, L, D, P)) {
+    if (sp.team.G > 1 && sp.team.nteam) {
+      // the re-dealt solve's tail teams: slots [0, K) as teams of G, the rest alone (K <= nteam_max on the device).
+      // Not cooperative: the grid exceeds the co-resident workgroups, but at most K (G - 1) < CUs members ever wait
+      // for a partner, and every other workgroup runs to its end without waiting, so each partner is dispatched
+      auto kt = integrate_kernel<NF, NT, L, D, P, true>;
+      hipError_t e = hipFuncSetAttribute((const void*)kt, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      if (e != hipSuccess) return e;
+      hipLaunchKernelGGL(kt, dim3(B + sp.team.nteam_max * (sp.team.G - 1)), dim3(Geo<NF, NT, P>::NTHR), lds, stream,
+                         net, sp, y0, feat, eps, y1, dlogp, nfe, status, B);
+      return hipGetLastError();
+    }
     if (sp.team.G > 1) {
     // team mode: the G members of a molecule wait on each other, so the launch must be co-resident; the cooperative
     // launch checks the grid against the occupancy query (hipErrorCooperativeLaunchTooLarge instead of a hang)

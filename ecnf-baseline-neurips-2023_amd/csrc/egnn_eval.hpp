@@ -1872,17 +1872,24 @@ __device__ __forceinline__ void edge_tile_cols(const Net& net, const BlockW& bw,
 // ---------------------------------------------------------------------------------------------------
 struct TeamP {
   int G;               // workgroups per molecule (<= 1: off)
-  int slot;            // floats per exchange slot: N M (messages) + (EP / 32) M (continuation rows) + align4(N D)
+  int slot;            // floats per exchange slot: (1 + NT) N M (messages, tangent rows after the primal ones)
+                       // + (EP / 32) M (continuation rows of the split primal kernels) + (1 + NT) align4(N D)
   float* buf;          // [molecules][2][G][slot]
   unsigned* ctr;       // [molecules] arrival counters (zeroed before every launch)
   int* timeout;        // [molecules] set when an exchange timed out (zeroed before every launch)
   int cols;            // 1: column-split mode (edge_tile_cols; G = tiles per molecule, one tile per member)
+  // teamed slots (device memory, nullptr: every slot): slots [0, *nteam) run as teams of G workgroups (blocks
+  // [0, G *nteam)), the slots after them alone, one workgroup each (the re-dealt adaptive solve's tail teams,
+  // ecnf_hip.hip redeal_kernel)
+  const int* nteam;
+  int nteam_max;       // host bound of *nteam (the launch's grid: B + nteam_max (G - 1) workgroups)
 };
 
 struct TeamCtx {
   TeamP p;
   int r;               // this workgroup's rank in its team
-  int T;               // the team's molecule
+  int T;               // the team's molecule slot
+  int G;               // workgroups of this slot's team (1: the slot runs alone, no exchange)
 };
 
 typedef ECNF_GLOBAL unsigned* gu32_p;
@@ -1890,11 +1897,16 @@ typedef ECNF_GLOBAL unsigned* gu32_p;
 // one exchange of the edge aggregates (MPW = 1; all threads of the workgroup, after the edge phase's barrier)
 template <int NT, int NTHR>
 __device__ __forceinline__ void team_exchange(const Net& net, const Lds& s, const TeamCtx& tm, int epoch) {
-  static_assert(NT == 0, "team mode runs the primal kernels");
+  const int G = tm.G;
+  if (G <= 1) return;   // a slot that runs alone holds every aggregate already
   const int tid = opaque_tid();
-  const int N = net.N, M = net.M, D = net.D, G = tm.p.G, r = tm.r, nn1 = N - 1, SR = net.SR;
+  const int N = net.N, M = net.M, D = net.D, r = tm.r, nn1 = N - 1, SR = net.SR, RP = net.RP;
   const int tpm = net.EP >> 5, M4 = M >> 2;
-  const int off_x = N * M, off_d = N * M + tpm * M;
+  // slot layout: messages [1 + NT][N][M] (tangent rows after the primal rows), continuation rows [tpm][M] (split
+  // primal kernels), shift rows [1 + NT][N][D] (tangent after primal).  The tangent kernels aggregate with LDS atomics
+  // (no continuation rows), so a receiver's primal and tangent rows come from the same one or two members.
+  const int off_x = (1 + NT) * N * M, off_d = off_x + tpm * M;
+  const int ND = N * D, ND4 = (ND + 3) & ~3;   // shift rows [1 + NT][ND4]: whole 16-B stores inside the slot
   float* base = tm.p.buf + ((size_t)tm.T * 2 + (epoch & 1)) * G * tm.p.slot;
   const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, 0x7fffffff, 0x00020000);
   const int mine = r * tm.p.slot * 4;   // byte offset of this member's slot
@@ -1904,19 +1916,23 @@ __device__ __forceinline__ void team_exchange(const Net& net, const Lds& s, cons
   auto first_tile = [&](int i) { return (i * SR) >> 5; };
   auto last_tile = [&](int i) { return (i * SR + nn1 - 1) >> 5; };
   // ---- publish the rows this member owns
-  for (int idx = tid; idx < N * M4; idx += NTHR) {
-    const int i = idx / M4, c = (idx - i * M4) * 4;
-    if (first_tile(i) % G == r) st16(i * M + c, *reinterpret_cast<const f32x4*>(s.macc + i * s.ld_m + c));
-    if (!net.cross && last_tile(i) != first_tile(i) && last_tile(i) % G == r)   // the receiver's second part
-      st16(i * M + c, *reinterpret_cast<const f32x4*>(s.macc + i * s.ld_m + c));
+  for (int idx = tid; idx < (1 + NT) * N * M4; idx += NTHR) {
+    const int w = idx / (N * M4), iw = idx - w * (N * M4);   // w = 1: the tangent row RP + i
+    const int i = iw / M4, c = (iw - i * M4) * 4;
+    const bool own = first_tile(i) % G == r ||
+                     (!net.cross && last_tile(i) != first_tile(i) && last_tile(i) % G == r);   // (its second part)
+    if (own) st16((w * N + i) * M + c, *reinterpret_cast<const f32x4*>(s.macc + (w * RP + i) * s.ld_m + c));
   }
   if (net.cross)
     for (int idx = tid; idx < tpm * M4; idx += NTHR) {
       const int t = idx / M4, c = (idx - t * M4) * 4;
       if (t % G == r) st16(off_x + t * M + c, *reinterpret_cast<const f32x4*>(s.cross + t * s.ld_m + c));
     }
-  for (int idx = tid; idx < (N * D + 3) >> 2; idx += NTHR)   // every member: its whole (partial) shift rows
+  for (int idx = tid; idx < (ND + 3) >> 2; idx += NTHR)   // every member: its whole (partial) shift rows
     st16(off_d + 4 * idx, *reinterpret_cast<const f32x4*>(s.dxacc + 4 * idx));
+  if constexpr (NT)   // ... and the tangent shift rows (LDS rows RP .. RP + N - 1; RP D is a multiple of 4 floats)
+    for (int idx = tid; idx < (ND + 3) >> 2; idx += NTHR)
+      st16(off_d + ND4 + 4 * idx, *reinterpret_cast<const f32x4*>(s.dxacc + RP * D + 4 * idx));
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains its write-through stores
   __syncthreads();
   // ---- arrive, then wait for the whole team.  A timeout is sticky: once any member has flagged the molecule (a member
@@ -1950,7 +1966,7 @@ __device__ __forceinline__ void team_exchange(const Net& net, const Lds& s, cons
   // written through by other XCDs' workgroups, so every load is a memory round trip, and one per loop trip
   // serialised ~14 of them per exchange
   constexpr int kB = 8;
-  const int nmsg = N * M4, ntot = nmsg + (net.cross ? tpm * M4 : 0);
+  const int nmsg = (1 + NT) * N * M4, ntot = nmsg + (net.cross ? tpm * M4 : 0);
   for (int base = tid; base < ntot; base += kB * NTHR) {
     f32x4 v[kB];
 #pragma unroll
@@ -1958,11 +1974,12 @@ __device__ __forceinline__ void team_exchange(const Net& net, const Lds& s, cons
       const int idx = base + u * NTHR;
       v[u] = f32x4{0.f, 0.f, 0.f, 0.f};
       if (idx < nmsg) {
-        const int i = idx / M4, c = (idx - i * M4) * 4;
+        const int w = idx / (N * M4), iw = idx - w * (N * M4);
+        const int i = iw / M4, c = (iw - i * M4) * 4;
         const int o0 = first_tile(i) % G, o1 = last_tile(i) % G;
-        v[u] = ld16(o0, i * M + c);
+        v[u] = ld16(o0, (w * N + i) * M + c);
         // atomically accumulated parts (no cross rows): 0 + a + b, whichever member holds each (exact in any order)
-        if (!net.cross && o1 != o0) v[u] += ld16(o1, i * M + c);
+        if (!net.cross && o1 != o0) v[u] += ld16(o1, (w * N + i) * M + c);
       } else if (idx < ntot) {
         const int t = (idx - nmsg) / M4, c = (idx - nmsg - t * M4) * 4;
         v[u] = ld16(t % G, off_x + t * M + c);
@@ -1972,20 +1989,21 @@ __device__ __forceinline__ void team_exchange(const Net& net, const Lds& s, cons
     for (int u = 0; u < kB; ++u) {
       const int idx = base + u * NTHR;
       if (idx < nmsg) {
-        const int i = idx / M4, c = (idx - i * M4) * 4;
-        *reinterpret_cast<f32x4*>(s.macc + i * s.ld_m + c) = v[u];
+        const int w = idx / (N * M4), iw = idx - w * (N * M4);
+        const int i = iw / M4, c = (iw - i * M4) * 4;
+        *reinterpret_cast<f32x4*>(s.macc + (w * RP + i) * s.ld_m + c) = v[u];
       } else if (idx < ntot) {
         const int t = (idx - nmsg) / M4, c = (idx - nmsg - t * M4) * 4;
         *reinterpret_cast<f32x4*>(s.cross + t * s.ld_m + c) = v[u];
       }
     }
   }
-  for (int idx = tid; idx < N * D; idx += NTHR) {
-    const int i = idx / D;
+  for (int idx = tid; idx < (1 + NT) * ND; idx += NTHR) {
+    const int w = idx / ND, iw = idx - w * ND, i = iw / D;
     const int o0 = first_tile(i) % G, o1 = last_tile(i) % G;
-    float v = slot0[(size_t)o0 * tm.p.slot + off_d + idx];
-    if (o1 != o0) v += slot0[(size_t)o1 * tm.p.slot + off_d + idx];
-    s.dxacc[idx] = v;
+    float v = slot0[(size_t)o0 * tm.p.slot + off_d + w * ND4 + iw];
+    if (o1 != o0) v += slot0[(size_t)o1 * tm.p.slot + off_d + w * ND4 + iw];
+    s.dxacc[w * RP * D + iw] = v;
   }
   __syncthreads();
 }
@@ -2006,7 +2024,8 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
   // not compiled for the L = 2 shapes (M, D) = (128, 3), (64, 2), where the primal tile's code beside the dual
   // tile's spilled 36 B per lane (tests/test_kernel_resources.py).  The BASELINE shapes (LJ13 128/3/3, ALDP 64/2/3,
   // DW4 128/3/2) have it.
-  constexpr bool kSparseX = Geo<NF, NT, P, BN>::kL2T && !(L == 2 && (NF == 4 || D == 2));
+  // (team kernels: tangent teams run Hutchinson solves only, ecnf_hip.hip team_size)
+  constexpr bool kSparseX = Geo<NF, NT, P, BN>::kL2T && !(L == 2 && (NF == 4 || D == 2)) && !TEAM;
   const int tid = opaque_tid(), lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: task indices stay in SGPRs
   const int N = net.N, H = net.H, T = net.T, M = NF * 32, RP = net.RP, MPW = net.MPW, ND = net.ND;
@@ -2141,7 +2160,7 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
       const int nd = nact * ndt;
       const int nrun = nd + (pload ? 0 : nact * tpm);
       // team mode (MPW = 1): this member runs tiles t = r, r + G, ... of the molecule (team_exchange)
-      const int tstep = TEAM ? tm->p.G : 1, tfirst = TEAM ? tm->r : 0;
+      const int tstep = TEAM ? tm->G : 1, tfirst = TEAM ? tm->r : 0;
       if constexpr (COLS) {
         // column-split team mode: member r runs tile r (G = tiles per molecule) with all of its waves
         static_assert(TEAM && NT == 0 && Geo<NF, NT, P, BN>::kSplit, "cols mode: team primal split kernels");

@@ -131,8 +131,11 @@ int ecnf_integrate(ecnf_handle* h, const ecnf_solve_opts* opts, const float* y0,
  * Adaptive (Dopri5 + PID) solves of 2 .. 2^20 molecules also use it, after the exact trace's cache, for the re-deal
  * scratch: when the batch needs more workgroups than the device has CUs, a first launch runs every molecule for a
  * few steps and stores its solver state, and a second launch resumes the unfinished molecules longest estimated
- * remainder first, so the slow molecules do not start late in dispatch order (ALDP B = 512 PID log_prob: ~44 ms vs
- * ~55 ms).  Bitwise the same results; a workspace too small for both regions runs the solve in one launch.
+ * remainder first, so the slow molecules do not start late in dispatch order (ALDP B = 512 PID log_prob: ~43 ms vs
+ * ~53 ms).  Where the shape has a tangent team kernel (ALDP's M = 64 network, one molecule per workgroup), the second
+ * launch of a Hutchinson solve also runs its longest-estimate eighth of the molecules (at most 64) as teams of two
+ * workgroups (ecnf_set_team below; ~38 ms).  Bitwise the same results; a workspace too small for both regions runs
+ * the solve in one launch.
  *   ecnf_integrate_workspace_size  bytes a call with these options and batch needs (0: none is used)
  *   ecnf_integrate_ws              ecnf_integrate with a CALLER-owned device workspace (NULL: none); the workspace is
  *                                  used stream-ordered on `stream` only, so concurrent calls with distinct
@@ -163,9 +166,12 @@ int ecnf_set_exact_form(ecnf_handle* h, int32_t form);
  * G workgroups integrate one molecule together, its edge tiles dealt over them, the edge aggregates exchanged through
  * global memory after every block's edge phase (a cooperative launch of batch x G workgroups).  Results are bitwise
  * those of the batch path.  mode: 0 auto (G = ceil(edge tiles / waves) when M = 256, batch x G <= CUs and
- * batch <= 32), 1 off, G >= 2 forced (capped by the handle's buffers).  ecnf_team_workgroups reports the G a solve of
- * `batch` molecules would use (1: the batch path).  A team whose exchange times out (a member not co-resident)
- * reports status ECNF_E_HIP for its molecule. */
+ * batch <= 32), 1 off (also turns off the re-dealt solves' tail teams), G >= 2 forced (batch <= 64, capped by the
+ * handle's buffers).  Hutchinson tangent solves (get_log_prob / sample_and_log_prob_cnf with approx=True) of ALDP's
+ * M = 64 network have a team kernel too (the tangent message and shift rows are exchanged as well), used when forced
+ * and for the re-dealt solves' tail teams; the exact trace always takes the batch path.  ecnf_team_workgroups reports
+ * the G a solve of `batch` molecules would use (1: the batch path; with_tangent: a Hutchinson solve).  A team whose
+ * exchange times out (a member not co-resident) reports status ECNF_E_HIP for its molecule. */
 int ecnf_set_team(ecnf_handle* h, int32_t mode);
 int ecnf_team_workgroups(ecnf_handle* h, int32_t with_tangent, int32_t batch, int32_t* G);
 

@@ -113,3 +113,37 @@ def test_team_qm9_one_molecule_vs_oracle_and_surface():
     assert float(np.abs(x1.cpu().numpy() - ref[0]).max()) <= 1e-4
     y, _, nfe, st = h.integrate(g(x0), g(feat, torch.int32), 0.0, 1.0, SolveOptions("dopri5", None))
     assert int(st[0]) == _lib.ECNF_OK and int(nfe[0]) > 7
+
+
+@pytest.mark.parametrize("B,mode,opts", [
+    (1, 2, SolveOptions("euler", 0.1)),
+    (5, 4, SolveOptions("euler", 0.1)),
+    (3, 3, SolveOptions("dopri5", None)),
+    (13, 4, SolveOptions("dopri5", None)),   # two groups of XCD-placed teams (8 + 5)
+])
+def test_tangent_team_bitwise_equals_batch_path(B, mode, opts):
+    """Team mode of the Hutchinson tangent kernels (ALDP's M = 64 shape, forced G; team_exchange also rebuilds the
+    tangent message and shift rows): get_log_prob (t = 1 -> 0) is bitwise the batch path's -- y(0), the divergence
+    integral, NFE and status.  The exact trace never runs in team mode (its sparse blocks are not exchanged): with a
+    forced G it takes the batch path, bitwise too."""
+    cfg = CONFIGS["aldp"]
+    oc, params, h, z, x0, feat = setup(cfg, B=B)
+    eps = g(np.asarray(z, np.float32))
+
+    def run(m, div):
+        h.set_team(m)
+        try:
+            return h.integrate(g(x0), g(feat, torch.int32), 1.0, 0.0, opts, div, eps if div == _lib.DIV_HUTCHINSON
+                               else None)
+        finally:
+            h.set_team(0)
+
+    h.set_team(mode)
+    assert h.team_workgroups(B, with_tangent=True) == mode
+    h.set_team(0)
+    assert h.team_workgroups(B, with_tangent=True) == 1   # tangent teams only when forced (or as re-deal tails)
+    for div in (_lib.DIV_HUTCHINSON,) + ((_lib.DIV_EXACT,) if opts.step_size else ()):
+        t, b = run(mode, div), run(1, div)
+        for p, q in zip(t, b):
+            assert torch.equal(p, q), (div, float((p.float() - q.float()).abs().max()))
+        assert int(t[3].abs().sum()) == 0
