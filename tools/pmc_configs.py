@@ -42,10 +42,13 @@ def main(prof):
         stats = [r for r in allstats if "integrate_kernel" in r["Name"]]
         # a re-dealt adaptive solve (ecnf_hip.hip redeal_kernel) is two integrate launches: every per-launch figure
         # below is per SOLVE, summed over its launches
+        # (the two launches may be different instantiations: the second one of an ALDP Hutchinson solve is the team
+        # kernel with its tail teams; the per-solve time is the sum over every integrate row / the solves)
         per = 2 if any("redeal_kernel" in r["Name"] for r in allstats) else 1
-        kt_avg_ms = float(stats[0]["AverageNs"]) * 1e-6 * per if stats else None
+        calls = sum(int(r["Calls"]) for r in stats)
+        kt_avg_ms = sum(float(r["TotalDurationNs"]) for r in stats) * 1e-6 / (calls // per) if stats else None
         rec = {"case": case, "bench_ms": line["ms"], "tflops": line["tflops"], "nfe_mean": line["nfe_mean"],
-               "rocprof_avg_ms": kt_avg_ms, "rocprof_calls": int(stats[0]["Calls"]) // per if stats else None,
+               "rocprof_avg_ms": kt_avg_ms, "rocprof_calls": calls // per if stats else None,
                "launches_per_solve": per, "frac_of_split_peak": line["tflops"] / PEAK_SPLIT}
         c0, d0 = per_dispatch(os.path.join(d, "p0"))
         c1, _ = per_dispatch(os.path.join(d, "p1"))
