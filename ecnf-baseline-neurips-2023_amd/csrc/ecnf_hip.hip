@@ -206,10 +206,13 @@ constexpr int kChunkSteps = 8;
 // PID Hutchinson log_prob from base draws 42.6 -> 37.7 ms (G = 4 with a makespan model choosing K = 26: 39.3 ms; G = 4,
 // K = 32: 39.7 ms); from real frames, whose long solves the 8-step estimate ranks worse, 49.8 -> 50.4 ms.
 constexpr int kTailG = 2;
+// Stop-and-team: the tail-team launch stops every molecule at its next step boundary once at most kStopLeft of its
+// slots are unfinished, and a third launch resumes the survivors as teams of kStopG (every CU in a team)
+constexpr int kStopG = 4;
 
 __global__ __launch_bounds__(kRedealThreads) void redeal_kernel(const float* __restrict__ state, int stride, int ND,
                                                                 int B, float tau1, int* order, int* nslots, float* gkey,
-                                                                int* gidx, int* nteam, int kmax) {
+                                                                int* gidx, int* nteam, int kmax, int team_all) {
   __shared__ float lkey[kRedealLds];
   __shared__ int lidx[kRedealLds];
   const int tid = threadIdx.x;
@@ -256,7 +259,10 @@ __global__ __launch_bounds__(kRedealThreads) void redeal_kernel(const float* __r
   if (tid == 0 && !(key[0] > -INFINITY)) *nslots = 0;
   if (!nteam) return;
   __syncthreads();
-  if (tid == 0) *nteam = min(kmax, (*nslots + 7) / 8);
+#ifndef ECNF_TAIL_DIV   // (experiment builds may override)
+#define ECNF_TAIL_DIV 8
+#endif
+  if (tid == 0) *nteam = min(kmax, team_all ? *nslots : (*nslots + ECNF_TAIL_DIV - 1) / ECNF_TAIL_DIV);
 }
 
 }  // namespace ecnf
@@ -682,7 +688,8 @@ int team_size(const ecnf_handle* h, int NT, int B, int* cols, int mode, int div 
 bool tail_teams(const ecnf_handle* h, int NT, int div, int mpw) {
   const ecnf_cfg& c = h->cfg;
   return NT == 1 && div == ECNF_DIV_HUTCHINSON && mpw == 1 && h->prec == 0 && h->team_buf.load() &&
-         h->team_mode.load() != 1 && kTailG <= h->team_gcap && team_shape(c.mlp_width, 1, c.mlp_depth, c.dim, 0);
+         h->team_mode.load() != 1 && kTailG <= h->team_gcap && kStopG <= h->team_gcap &&
+         team_shape(c.mlp_width, 1, c.mlp_depth, c.dim, 0);
 }
 
 // G, cols: team_size's decision for this solve (G = 1: the batch path)
@@ -752,7 +759,7 @@ hipError_t dispatch_integrate(const ecnf_handle* h, int NT, const SolveP& sp_in,
   const int kmax = tail ? std::min(h->team_cap, h->ncu / (2 * kTailG)) : 0;
   int* nteam = tail ? nslots + 1 : nullptr;
   hipLaunchKernelGGL(redeal_kernel, dim3(1), dim3(kRedealThreads), 0, stream, sched, stride, ND, B, sp.tau1, order,
-                     nslots, gkey, gidx, nteam, kmax);
+                     nslots, gkey, gidx, nteam, kmax, 0);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   SolveP s2 = sp;
@@ -770,8 +777,33 @@ hipError_t dispatch_integrate(const ecnf_handle* h, int NT, const SolveP& sp_in,
     s2.team.timeout = reinterpret_cast<int*>(h->team_sync + kTeamCap);
     s2.team.nteam = nteam;
     s2.team.nteam_max = kmax;
+    // stop-and-team: the molecules still unfinished once at most kstop are left go on in a third launch, all of
+    // them teams of kStopG
+#ifdef ECNF_STOP_LEFT   // (experiment builds)
+    const int kstop = ECNF_STOP_LEFT;
+#else
+    const int kstop = std::min(h->team_cap, h->ncu / kStopG);
+#endif
+    s2.team.fin = nslots + 2;
+    s2.team.nsl = nslots;
+    s2.team.stop_left = kstop;
     e = hipMemsetAsync(h->team_sync, 0, kTeamSyncBytes, stream);
     if (e != hipSuccess) return e;
+    e = hipMemsetAsync(s2.team.fin, 0, sizeof(int), stream);
+    if (e != hipSuccess) return e;
+    e = launch(s2);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(redeal_kernel, dim3(1), dim3(kRedealThreads), 0, stream, sched, stride, ND, B, sp.tau1, order,
+                       nslots, gkey, gidx, nteam, kstop, 1);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    SolveP s3 = s2;
+    s3.team.G = kStopG;
+    s3.team.nteam_max = kstop;
+    s3.team.fin = nullptr;
+    e = hipMemsetAsync(h->team_sync, 0, kTeamSyncBytes, stream);
+    if (e != hipSuccess) return e;
+    return launch(s3);
   }
   return launch(s2);
 }
@@ -1191,7 +1223,8 @@ int ecnf_create(const ecnf_cfg* cfg, const float* params, size_t n_floats, int d
     h->team_gcap = c.mlp_width == 256 ? tpm : std::min(tpm, std::max(4, (tpm + primal_waves(c) - 1) / primal_waves(c)));
     // (the tangent team kernels also exchange the tangent message and shift rows: egnn_eval.hpp team_exchange)
     const bool tan_team = team_shape(c.mlp_width, 1, c.mlp_depth, c.dim, 0);
-    h->team_slot = (tan_team ? 2 : 1) * (c.n_nodes * M + ((c.n_nodes * c.dim + 3) & ~3)) + tpm * M;
+    // (+ 4 floats: member 0's stop verdict, egnn_eval.hpp team_exchange)
+    h->team_slot = (tan_team ? 2 : 1) * (c.n_nodes * M + ((c.n_nodes * c.dim + 3) & ~3)) + tpm * M + 4;
     const size_t nb = (size_t)h->team_cap * 2 * h->team_gcap * h->team_slot * sizeof(float);
     const bool want = h->split_ok && (team_shape(c.mlp_width, 0, c.mlp_depth, c.dim, 0) || tan_team);
     float* tb = nullptr;
@@ -1339,6 +1372,8 @@ int ecnf_integrate_plan(ecnf_handle* h, const ecnf_solve_opts* o, int32_t batch,
   *workgroups = grid;
   *launches = (sched_floats(h, o, batch) > 0 && adaptive && grid > h->ncu &&
                chunkable(h->cfg.mlp_width / 32, NT, h->prec)) ? 2 : 1;
+  // (the re-dealt solve with tail teams adds the stop-and-team launch)
+  if (*launches == 2 && tail_teams(h, NT, o->divergence, net.MPW)) *launches = 3;
   return ECNF_OK;
 }
 

@@ -108,13 +108,7 @@ __device__ __forceinline__ float uniform_f(float x) {
   return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, x)));
 }
 
-// the solver loop's sizes (MPW, ND) and the LDS offset of the solver state, in static LDS: written once at the kernel's
-// start and read at every use site in the loop (LDS loads after barriers), so they occupy no SGPRs across the
-// evaluations (kept in SGPRs, they were spilled through VGPRs to scratch in the 256-register kernels)
-__device__ __forceinline__ int* solver_sizes() {
-  __shared__ int sz[4];   // [MPW, ND, solver-state offset in floats from the dynamic LDS base, -]
-  return sz;
-}
+// (solver_sizes(): egnn_eval.hpp)
 __device__ __forceinline__ int solver_size(int k) { return __builtin_amdgcn_readfirstlane(solver_sizes()[k]); }
 
 // tau1 passes an empty asm (wave-uniform) so the threshold tau1 - 1e-6 is formed at each use: hoisted out of the solver
@@ -245,6 +239,9 @@ __global__ __launch_bounds__((kernel_threads<NF, NT, P, COLS>())) __attribute__(
     }
   }
   const TeamCtx* tm = team ? &team_ctx : nullptr;
+  if constexpr (team) {
+    if (threadIdx.x == 0) *team_stop_flag() = 0;   // (stop-and-team: no verdict before the first exchange)
+  }
   int tepoch = 0;
   const bool writer_wg = team_ctx.r == 0;
   // launch slots slot0 .. slot0 + nmol - 1; slot j integrates batch molecule sp.order[j] (re-dealt solves) or j
@@ -365,11 +362,23 @@ __global__ __launch_bounds__((kernel_threads<NF, NT, P, COLS>())) __attribute__(
         if (tid == 0) {
           int any = 0;
           for (int m = 0; m < MPW; ++m) any |= st.active[m];
+          if constexpr (TEAM) {
+            // stop-and-team: stop at this step boundary once few molecules are left (a team: member 0's verdict from
+            // the last exchange, the same for every member)
+            if (sp.team.fin) {
+              const bool stop = team_ctx.G > 1 ? *team_stop_flag() != 0
+                                               : *sp.team.nsl - __hip_atomic_load((ECNF_GLOBAL int*)sp.team.fin,
+                                                                                  __ATOMIC_RELAXED,
+                                                                                  __HIP_MEMORY_SCOPE_AGENT) <=
+                                                     sp.team.stop_left;
+              if (stop) any |= 2;
+            }
+          }
           *st.any = any;
         }
         if (tid < MPW) st.h[tid] = st.tnext[tid] - st.tau[tid];
         __syncthreads();
-        if (*st.any == 0) break;
+        if ((*st.any & 1) == 0 || (*st.any & 2)) break;
         // chunked solve: stop at this step boundary once the launch has done its step controls (state stored below)
         const int chunk = chunkable(NF, NT, P) ? opaque_u(sp.chunk_steps) : 0;
         if (chunk > 0 && __builtin_amdgcn_readfirstlane(st.ctl[5]) >= chunk) break;
@@ -514,6 +523,10 @@ __global__ __launch_bounds__((kernel_threads<NF, NT, P, COLS>())) __attribute__(
             st.status[m] = ECNF_E_MAX_STEPS;
             st.active[m] = 0;
           }
+          if constexpr (TEAM) {   // stop-and-team: one count per finished molecule (its member 0)
+            if (sp.team.fin && !st.active[m] && team_ctx.r == 0)
+              __hip_atomic_fetch_add((ECNF_GLOBAL int*)sp.team.fin, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
         }
       }
       stage = 1;
@@ -545,7 +558,8 @@ __global__ __launch_bounds__((kernel_threads<NF, NT, P, COLS>())) __attribute__(
   {
   const int tid = opaque_tid();
   const SolverLds st = carve_solver(smem + solver_size(2), MPW, ND);
-  if (chunkable(NF, NT, P) && sp.chunk_steps > 0) {   // chunked solve: every molecule's state at this step boundary
+  // chunked solve (or a stop-and-team launch): every molecule's state at this step boundary
+  if (chunkable(NF, NT, P) && (sp.chunk_steps > 0 || (TEAM && sp.team.fin))) {
     for (int i = tid; i < nmol * ND; i += kThreads) {
       const int m = i / ND, c = i - m * ND;
       float* S = sp.state + (size_t)mol_index(sp.order, slot0, m) * sp.state_stride;

@@ -1883,7 +1883,25 @@ struct TeamP {
   // ecnf_hip.hip redeal_kernel)
   const int* nteam;
   int nteam_max;       // host bound of *nteam (the launch's grid: B + nteam_max (G - 1) workgroups)
+  // stop-and-team (the re-dealt solve's second launch, ecnf_hip.hip dispatch_integrate): *fin counts the molecules
+  // finished in this launch; once at most stop_left of the *nsl occupied slots are unfinished, every molecule stops at
+  // its next step boundary (state stored) and a third launch resumes the survivors as teams.  A team decides through
+  // its member 0, whose verdict travels in the exchange slot (team_stop_flag), so all members stop at the same step
+  int* fin;            // (nullptr: off)
+  const int* nsl;
+  int stop_left;
 };
+
+// the solver loop's sizes (MPW, ND), the LDS offset of the solver state, and a team's stop verdict (stop-and-team,
+// read from member 0's exchange slot at the last exchange), in static LDS: written once and read at every use site
+// (LDS loads after barriers), so they occupy no SGPRs across the evaluations (kept in SGPRs, they were spilled through
+// VGPRs to scratch in the 256-register kernels).  ONE 16-B array: a static LDS variable of another size would move
+// the dynamic LDS base off its 16-B alignment, and every ds_read_b128 of the carve-up with it
+__device__ __forceinline__ int* solver_sizes() {
+  __shared__ int sz[4];   // [MPW, ND, solver-state offset in floats from the dynamic LDS base, team stop verdict]
+  return sz;
+}
+__device__ __forceinline__ int* team_stop_flag() { return solver_sizes() + 3; }
 
 struct TeamCtx {
   TeamP p;
@@ -1907,6 +1925,7 @@ __device__ __forceinline__ void team_exchange(const Net& net, const Lds& s, cons
   // (no continuation rows), so a receiver's primal and tangent rows come from the same one or two members.
   const int off_x = (1 + NT) * N * M, off_d = off_x + tpm * M;
   const int ND = N * D, ND4 = (ND + 3) & ~3;   // shift rows [1 + NT][ND4]: whole 16-B stores inside the slot
+  const int off_f = off_d + (1 + NT) * ND4;    // member 0's stop verdict (stop-and-team), one 16-B chunk
   float* base = tm.p.buf + ((size_t)tm.T * 2 + (epoch & 1)) * G * tm.p.slot;
   const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, 0x7fffffff, 0x00020000);
   const int mine = r * tm.p.slot * 4;   // byte offset of this member's slot
@@ -1933,6 +1952,11 @@ __device__ __forceinline__ void team_exchange(const Net& net, const Lds& s, cons
   if constexpr (NT)   // ... and the tangent shift rows (LDS rows RP .. RP + N - 1; RP D is a multiple of 4 floats)
     for (int idx = tid; idx < (ND + 3) >> 2; idx += NTHR)
       st16(off_d + ND4 + 4 * idx, *reinterpret_cast<const f32x4*>(s.dxacc + RP * D + 4 * idx));
+  if (tm.p.fin && r == 0 && tid == 0) {   // stop-and-team: member 0's verdict for every member
+    const int left = *tm.p.nsl - __hip_atomic_load((ECNF_GLOBAL int*)tm.p.fin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const float v = left <= tm.p.stop_left ? 1.0f : 0.0f;
+    st16(off_f, f32x4{v, v, v, v});
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains its write-through stores
   __syncthreads();
   // ---- arrive, then wait for the whole team.  A timeout is sticky: once any member has flagged the molecule (a member
@@ -1955,6 +1979,7 @@ __device__ __forceinline__ void team_exchange(const Net& net, const Lds& s, cons
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
+  if (tm.p.fin && tid == 0) *team_stop_flag() = base[off_f] != 0.0f ? 1 : 0;   // member 0's slot (slot 0)
   __syncthreads();
   // ---- rebuild the aggregates a single workgroup would hold
   const float* slot0 = base;

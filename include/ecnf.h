@@ -134,8 +134,9 @@ int ecnf_integrate(ecnf_handle* h, const ecnf_solve_opts* opts, const float* y0,
  * remainder first, so the slow molecules do not start late in dispatch order (ALDP B = 512 PID log_prob: ~43 ms vs
  * ~53 ms).  Where the shape has a tangent team kernel (ALDP's M = 64 network, one molecule per workgroup), the second
  * launch of a Hutchinson solve also runs its longest-estimate eighth of the molecules (at most 64) as teams of two
- * workgroups (ecnf_set_team below; ~38 ms).  Bitwise the same results; a workspace too small for both regions runs
- * the solve in one launch.
+ * workgroups (ecnf_set_team below), stops every molecule at a step boundary once at most 64 are unfinished, and a
+ * third launch resumes those as teams of four (~36 ms).  Bitwise the same results; a workspace too small for both
+ * regions runs the solve in one launch.
  *   ecnf_integrate_workspace_size  bytes a call with these options and batch needs (0: none is used)
  *   ecnf_integrate_ws              ecnf_integrate with a CALLER-owned device workspace (NULL: none); the workspace is
  *                                  used stream-ordered on `stream` only, so concurrent calls with distinct
@@ -151,7 +152,7 @@ int ecnf_integrate_ws(ecnf_handle* h, const ecnf_solve_opts* opts, const float* 
 int ecnf_reserve_workspace(ecnf_handle* h, size_t bytes);
 /* Diagnostic: how a solve with these options and batch is launched when given a workspace of
  * ecnf_integrate_workspace_size bytes -- the workgroups of its (first) launch and the number of launches (2: the
- * chunked, re-dealt adaptive solve above; 1: one launch). */
+ * chunked, re-dealt adaptive solve above; 3: the same with tail teams and the stop-and-team launch; 1: one launch). */
 int ecnf_integrate_plan(ecnf_handle* h, const ecnf_solve_opts* opts, int32_t batch, int32_t* workgroups,
                         int32_t* launches);
 

@@ -87,3 +87,71 @@ def sim_policy(path, Gs=(2, 3, 4), Ks=(0, 8, 16, 24, 32, 40, 48, 56, 64)):
 
 for p in sys.argv[1:]:
     sim_policy(p)
+
+
+def sim_stop(path, thresholds=((64, 4),), tail=(2, 64), stop_cost=6.0):
+    """launch 2 (optionally with tail teams) stopped when at most `n` molecules remain unfinished, then a launch with
+    the survivors as teams of G (G x n <= CUs), possibly again at the next threshold; stop_cost: evaluations lost per
+    stop (the molecules finish their current step)"""
+    d = np.load(path)
+    key, nfe1, nfe = d["key"], d["nfe1"], d["nfe"]
+    idx = np.nonzero(key >= 0)[0]
+    order = idx[np.lexsort((idx, -key[idx]))]
+    rem = {int(m): float(nfe[m] - nfe1[m]) for m in idx}
+    l1 = schedule([(1, float(n)) for n in np.minimum(nfe1, nfe)])
+    # event simulation of launch 2: (start, end) per molecule on a heap of CUs
+    G2, K2 = tail
+    jobs = [(G2 if k < K2 else 1, m) for k, m in enumerate(order)]
+    free = [0.0] * NCU
+    heapq.heapify(free)
+    spans = {}
+    for cus, m in jobs:
+        starts = [heapq.heappop(free) for _ in range(cus)]
+        t0 = max(starts)
+        dur = rem[m] / SPEED[cus]
+        for _ in range(cus):
+            heapq.heappush(free, t0 + dur)
+        spans[m] = (t0, t0 + dur, cus)
+    t = 0.0
+    out = []
+    ends = sorted(e for _, e, _ in spans.values())
+    n_all = len(ends)
+    done_rem = {}
+    total = l1
+    cur = dict(spans)
+    prev_t = 0.0
+    for n_th, G in thresholds:
+        if n_all <= n_th:
+            break
+        t_stop = ends[n_all - n_th - 1]   # the time the (n_all - n_th)-th molecule finishes
+        surv = {}
+        for m, (s0, e0, cus) in cur.items():
+            if e0 > t_stop:
+                done = max(0.0, t_stop - s0) * SPEED[cus]
+                surv[m] = rem[m] - done + stop_cost
+        total += t_stop
+        # next launch: survivors as teams of G, all concurrent
+        ends = sorted(v / SPEED[G] for v in surv.values())
+        rem = surv
+        cur = {m: (0.0, v / SPEED[G], G) for m, v in surv.items()}
+        n_all = len(ends)
+        out.append((n_th, G, round(t_stop), len(surv)))
+    total += max(e for _, e, _ in cur.values())
+    print(f"  {path}: tail {tail} stops {thresholds}: {total:.0f}  {out}")
+
+
+for p in sys.argv[1:]:
+    for th in (((64, 4),), ((128, 2),), ((128, 2), (64, 4)), ((96, 2),), ((32, 4),)):
+        for tail in ((2, 64), (1, 0)):
+            sim_stop(p, th, tail)
+
+
+def sweep(paths):
+    for tail in ((1, 0), (2, 16), (2, 32), (2, 64), (4, 16), (4, 32), (3, 32)):
+        for th in (((64, 4),), ((48, 4),), ((80, 3),), ((96, 2), (48, 4))):
+            for p in paths:
+                sim_stop(p, th, tail)
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "--sweep":
+    sweep(sys.argv[2:])
