@@ -44,8 +44,10 @@ def main(prof):
         # below is per SOLVE, summed over its launches
         # (the two launches may be different instantiations: the second one of an ALDP Hutchinson solve is the team
         # kernel with its tail teams; the per-solve time is the sum over every integrate row / the solves)
-        per = 2 if any("redeal_kernel" in r["Name"] for r in allstats) else 1
+        # tools/profile_configs.sh runs each case as 1 warm-up + 2 timed solves (bench_paths --reps 2): the launches
+        # per solve are the integrate launches / 3 (1; 2: re-dealt; 3: with ALDP's tail teams and stop-and-team)
         calls = sum(int(r["Calls"]) for r in stats)
+        per = max(1, calls // 3)
         kt_avg_ms = sum(float(r["TotalDurationNs"]) for r in stats) * 1e-6 / (calls // per) if stats else None
         rec = {"case": case, "bench_ms": line["ms"], "tflops": line["tflops"], "nfe_mean": line["nfe_mean"],
                "rocprof_avg_ms": kt_avg_ms, "rocprof_calls": calls // per if stats else None,
