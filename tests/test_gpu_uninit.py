@@ -97,3 +97,32 @@ def test_redealt_adaptive_solve_does_not_depend_on_stale_state(poison):
         assert torch.equal(p, q)
     assert int(outs[0][2].abs().sum()) == 0 and bool(torch.isfinite(outs[0][0]).all())
     h.close()
+
+
+@pytest.mark.timeout(240)
+def test_stop_and_team_solve_does_not_depend_on_stale_state(poison):
+    """The three-launch Hutchinson log_prob: the tail-team second launch stops early and the third launch
+    resumes every survivor as a team of four, each member zero-filling its eval and solver LDS before it loads the stored
+    state and tangent rows.  ALDP B = 512 PID Hutchinson, asserted three launches, bitwise equal under a zero and a NaN
+    fill."""
+    cfg = CONFIGS["aldp"]
+    h = EcnfHandle(cfg, init_params(cfg, 0), 0)
+    B = 512
+    opts = SolveOptions("dopri5", None)
+    wg, launches = h.integrate_plan(B, 1.0, 0.0, opts, _lib.DIV_HUTCHINSON)
+    assert launches == 3, (wg, launches)
+    g = torch.Generator("cuda").manual_seed(11)
+    z = torch.randn((B, cfg.event_dim), device="cuda", generator=g)
+    x = h.base_sample(z)
+    feat = (torch.arange(cfg.n_nodes, device="cuda", dtype=torch.int32) % cfg.n_features).expand(B, -1).contiguous()
+    eps = torch.randn((B, cfg.event_dim), device="cuda", generator=g)
+    outs = []
+    for bits in (0x00000000, 0x7FC00000):
+        poison(bits)
+        y, dl, nfe, st = h.integrate(x, feat, 1.0, 0.0, opts, _lib.DIV_HUTCHINSON, eps, check_status=False)
+        torch.cuda.synchronize()
+        outs.append((y, dl, nfe, st))
+    for p, q in zip(*outs):
+        assert torch.equal(p, q)
+    assert int(outs[0][3].abs().sum()) == 0 and bool(torch.isfinite(outs[0][1]).all())
+    h.close()
