@@ -208,7 +208,11 @@ constexpr int kChunkSteps = 8;
 constexpr int kTailG = 2;
 // Stop-and-team: the tail-team launch stops every molecule at its next step boundary once at most kStopLeft of its
 // slots are unfinished, and a third launch resumes the survivors as teams of kStopG (every CU in a team)
+#ifdef ECNF_STOP_G   // (experiment builds)
+constexpr int kStopG = ECNF_STOP_G;
+#else
 constexpr int kStopG = 4;
+#endif
 
 __global__ __launch_bounds__(kRedealThreads) void redeal_kernel(const float* __restrict__ state, int stride, int ND,
                                                                 int B, float tau1, int* order, int* nslots, float* gkey,
@@ -756,7 +760,11 @@ hipError_t dispatch_integrate(const ecnf_handle* h, int NT, const SolveP& sp_in,
   // tail teams (kTailG workgroups for the longest slots) where the shape has a tangent team kernel and the batch runs
   // one molecule per workgroup; the caller holds team_mu (integrate_impl) and the team buffers are this solve's
   const bool tail = tail_teams(h, NT, sp.div, net.MPW);
+#ifdef ECNF_TAIL_KMAX   // (experiment builds)
+  const int kmax = tail ? ECNF_TAIL_KMAX : 0;
+#else
   const int kmax = tail ? std::min(h->team_cap, h->ncu / (2 * kTailG)) : 0;
+#endif
   int* nteam = tail ? nslots + 1 : nullptr;
   hipLaunchKernelGGL(redeal_kernel, dim3(1), dim3(kRedealThreads), 0, stream, sched, stride, ND, B, sp.tau1, order,
                      nslots, gkey, gidx, nteam, kmax, 0);
@@ -1202,6 +1210,10 @@ int ecnf_create(const ecnf_cfg* cfg, const float* params, size_t n_floats, int d
       set_mpw(n, c, NT, P, mpw, rp);
       n.lds_floats = (int)(lds / 4);
       h->lds[ix] = lds;
+      // block-1 pair tiles (egnn_eval.hpp PairPlan13): one node feature (every atom's block-1 h is the same), 13 atoms,
+      // the M = 128 split primal kernels (8 waves, each with a 1024-float slice of the >= 32 x 260-float P rows)
+      n.pairs = (NT == 0 && P == 0 && split_primal(c, 0, 0) && c.n_features == 1 && c.n_nodes == 13 &&
+                 c.mlp_width == 128 && primal_waves(c) * 1024 <= 32 * 260) ? 1 : 0;
     } else {
       n.MPW = 0;
       h->lds[ix] = 0;

@@ -174,6 +174,7 @@ struct Net {
   int cross;      // split kernels: message segment parts are stored, not atomically added (Lds::cross)
   int wide;       // M = 128 tangent kernels in the wide form (Geo BN: per-edge phi_e.0, no P rows; 34 .. 64 atoms)
   int ncross;     // receiver segments per molecule that cross a tile boundary (split kernels with cross)
+  int pairs;      // block-1 pair tiles (PairPlan13: one node feature, N = 13, the M = 128 split primal kernels)
   unsigned char xs_i[kMaxTilesPerMol];   // ... their receiver atom i
   unsigned char xs_t[kMaxTilesPerMol];   // ... and the molecule tile that holds their continuation part
   float freqs[kMaxHalfT];
@@ -935,6 +936,201 @@ __device__ __forceinline__ void lds_dot(const float* __restrict__ w, const f32x1
   dT = NT ? (pt[0] + pt[1]) + (pt[2] + pt[3]) : 0.f;
 }
 
+// ---------------------------------------------------------------------------------------------------
+// Block-1 pair tiles (single-feature molecules of 13 atoms, e.g. LJ13; the M = 128 split primal kernels).  With one
+// node feature every atom enters block 1 with the same h (the embedding of that feature and the time, egnn.py:162-167),
+// so phi_e's input [h_s, h_r, |r|^2] (egnn.py:76) is symmetric: m_ij = m_ji BITWISE (|r_ji| = |r_ij| exactly and the
+// per-node phi_e.0 halves P_s, P_r are equal rows), and so are the gate and phi_x (egnn.py:82-101).  Block 1 then runs
+// the chains once per unordered pair, 78 pairs in 3 tiles instead of 156 edges in 5, and adds each pair's gated
+// message to both atoms and its shift with opposite signs (r_ji = -r_ij).  Tiles over the groups A = {0..3},
+// B = {4..7}, C = {8..12}: tile 0 = the pairs inside A u B (28), tile 1 = A x C and inside C (30), tile 2 = B x C (20),
+// so every atom sits in exactly two tiles and gets two atomic contributions per block (0 + a + b, exact in either
+// order, as the receiver segments' two parts: run-to-run deterministic and independent of the molecules per
+// workgroup).  Inside a tile an atom's pairs sit on several lanes: the wave transposes its gated messages through a
+// 1024-float slice of the P rows (dead once layer 1 read its per-molecule rows, copied before the edge phase) and sums
+// each atom's pairs in a fixed order.
+// ---------------------------------------------------------------------------------------------------
+struct PairPlan13 {
+  static constexpr int kN = 13, kTiles = 3, kMaxNodes = 9, kMaxDeg = 8;
+  struct Tile {
+    int np;                      // pairs (lanes np .. 31 are padding)
+    unsigned char a[32], b[32];  // pair (a, b), a < b: r = x_a - x_b; +m, +shift to a and +m, -shift to b
+    int nn;                      // atoms touched
+    unsigned char node[kMaxNodes], deg[kMaxNodes], lane[kMaxNodes][kMaxDeg], role[kMaxNodes][kMaxDeg];
+  };
+  static constexpr Tile make(int t) {
+    Tile x{};
+    auto add = [&](int a, int b) {
+      x.a[x.np] = (unsigned char)a;
+      x.b[x.np] = (unsigned char)b;
+      ++x.np;
+    };
+    if (t == 0) {
+      for (int a = 0; a < 8; ++a)
+        for (int b = a + 1; b < 8; ++b) add(a, b);
+    } else if (t == 1) {
+      for (int a = 0; a < 4; ++a)
+        for (int b = 8; b < 13; ++b) add(a, b);
+      for (int a = 8; a < 13; ++a)
+        for (int b = a + 1; b < 13; ++b) add(a, b);
+    } else {
+      for (int a = 4; a < 8; ++a)
+        for (int b = 8; b < 13; ++b) add(a, b);
+    }
+    for (int n = 0; n < kN; ++n) {
+      int d = 0;
+      for (int p = 0; p < x.np; ++p)
+        if (x.a[p] == n || x.b[p] == n) {
+          x.lane[x.nn][d] = (unsigned char)p;
+          x.role[x.nn][d] = x.b[p] == n ? 1 : 0;
+          ++d;
+        }
+      if (d) {
+        x.node[x.nn] = (unsigned char)n;
+        x.deg[x.nn] = (unsigned char)d;
+        ++x.nn;
+      }
+    }
+    return x;
+  }
+  // the two tiles that hold atom n's pairs (team_exchange's owners)
+  __host__ __device__ __forceinline__ static constexpr int tile_lo(int n) { return n < 8 ? 0 : 1; }
+  __host__ __device__ __forceinline__ static constexpr int tile_hi(int n) { return n < 4 ? 1 : 2; }
+  // lane word w (lanes 8w .. 8w+7) of tile t: bytes a | b << 4, 0xFF on padding lanes
+  static constexpr unsigned long long word(int t, int w) {
+    const Tile x = make(t);
+    unsigned long long v = 0;
+    for (int e = 0; e < 8; ++e) {
+      const int p = 8 * w + e;
+      const unsigned long long byte = p < x.np ? (unsigned long long)(x.a[p] | (x.b[p] << 4)) : 0xFFull;
+      v |= byte << (8 * e);
+    }
+    return v;
+  }
+};
+static_assert(PairPlan13::make(0).np == 28 && PairPlan13::make(1).np == 30 && PairPlan13::make(2).np == 20 &&
+              PairPlan13::make(0).nn == 8 && PairPlan13::make(1).nn == 9 && PairPlan13::make(2).nn == 9,
+              "pair tiles of a 13-atom molecule");
+
+// this lane's pair code (a | b << 4, 0xFF: padding) in pair tile tp (wave-uniform)
+__device__ __forceinline__ unsigned pair13_code(int tp, int li) {
+  // (the words as constants: PairPlan13::word called with a runtime tile compiled to real function calls)
+  unsigned long long w[4];
+  static_for<4>([&](auto Wc) {
+    constexpr int q = decltype(Wc)::value;
+    constexpr unsigned long long w0 = PairPlan13::word(0, q), w1 = PairPlan13::word(1, q), w2 = PairPlan13::word(2, q);
+    w[q] = tp == 0 ? w0 : tp == 1 ? w1 : w2;
+  });
+  const int h = li >> 3;
+  const unsigned long long v = h == 0 ? w[0] : h == 1 ? w[1] : h == 2 ? w[2] : w[3];
+  return (unsigned)(v >> (8 * (li & 7))) & 0xFFu;
+}
+
+// per-pair context of a block-1 pair tile, passed by value (sb == nullptr: the receiver-segment path; a pointer to a
+// local context kept it in scratch, and its LDS pointers became flat ones)
+struct PairCtx {
+  int mol;     // molecule slot in the workgroup
+  int tp;      // pair tile of the molecule (0 .. 2)
+  float* sb;   // this wave's 1024-float transposition slice (16-B aligned)
+};
+
+// m_i += sum over atom i's pairs of m e (egnn.py:102-104) for pair tile TP: per pass two 32-feature blocks, the tile's
+// pairs in two halves of 16 LDS rows of 64 features (16-B chunks XOR-swizzled by row: conflict-free column reads), then
+// lane c sums feature c over each atom's pairs (fixed order) and adds it to macc
+template <int TP, int NF>
+__device__ __forceinline__ void pair_agg_tile(const Lds& s, const f32x16 (&m)[NF], float g, int mol, float* sb,
+                                              int lane) {
+  constexpr PairPlan13::Tile T = PairPlan13::make(TP);
+  const int kk = lane >> 5, li = lane & 31, ch = lane >> 2, e = lane & 3;
+  float* mrows = s.macc + mol * PairPlan13::kN * s.ld_m + lane;
+  static_for<NF / 2>([&](auto Pc) {
+    constexpr int pass = decltype(Pc)::value;
+    float acc[T.nn];
+    static_for<2>([&](auto Hc) {
+      constexpr int h = decltype(Hc)::value;
+      if ((li >> 4) == h) {
+        const int p = li & 15;
+        static_for<2>([&](auto Fc) {
+          constexpr int fbl = decltype(Fc)::value, fb = 2 * pass + fbl;
+          static_for<4>([&](auto Qc) {
+            constexpr int q = decltype(Qc)::value;
+            const int c16 = fbl * 8 + 2 * q + kk;   // features 8q + 4kk .. +3 of block fb (accumulator rows 4q .. 4q+3)
+            *reinterpret_cast<f32x4*>(sb + p * 64 + ((c16 ^ p) << 2)) =
+                f32x4{m[fb][4 * q] * g, m[fb][4 * q + 1] * g, m[fb][4 * q + 2] * g, m[fb][4 * q + 3] * g};
+          });
+        });
+      }
+      // the wave's own LDS traffic runs in order; keep the compiler from moving the column reads above the stores (or
+      // the next half's stores above these reads), and each atom's reads together (register pressure)
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      static_for<T.nn>([&](auto Sc) {
+        constexpr int sl = decltype(Sc)::value;
+        float v;
+        if constexpr (h == 0) v = 0.f;
+        else v = acc[sl];
+        static_for<T.deg[sl]>([&](auto Qc) {
+          constexpr int p = T.lane[sl][decltype(Qc)::value];
+          if constexpr ((p >> 4) == h) v += sb[(p & 15) * 64 + ((ch ^ (p & 15)) << 2) + e];
+        });
+        acc[sl] = v;
+        __builtin_amdgcn_sched_barrier(0);
+      });
+      asm volatile("" ::: "memory");
+    });
+    static_for<T.nn>([&](auto Sc) {
+      constexpr int sl = decltype(Sc)::value;
+      lds_add(mrows + T.node[sl] * s.ld_m + pass * 64, acc[sl]);
+    });
+  });
+}
+
+// shift_i += sum over atom i's pairs of +-phi_x r / (C + |r|) (egnn.py:87-94) for pair tile TP: rows of 8 floats
+// [+shift | -shift], lanes d < D sum each atom's pairs (fixed order)
+template <int TP, int D>
+__device__ __forceinline__ void pair_shift_tile(const Lds& s, const float (&sh)[D], int mol, float* sb, int lane) {
+  static_assert(D <= 4, "one 16-B half row per sign");
+  constexpr PairPlan13::Tile T = PairPlan13::make(TP);
+  const int kk = lane >> 5, li = lane & 31;
+  if (kk == 0) {
+    f32x4 pv = {0.f, 0.f, 0.f, 0.f}, nv = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      pv[d] = sh[d];
+      nv[d] = -sh[d];
+    }
+    *reinterpret_cast<f32x4*>(sb + li * 8) = pv;
+    *reinterpret_cast<f32x4*>(sb + li * 8 + 4) = nv;
+  }
+  asm volatile("" ::: "memory");
+  if (lane < D) {
+    static_for<T.nn>([&](auto Sc) {
+      constexpr int sl = decltype(Sc)::value;
+      float v = 0.f;
+      static_for<T.deg[sl]>([&](auto Qc) {
+        constexpr int q = decltype(Qc)::value;
+        v += sb[T.lane[sl][q] * 8 + T.role[sl][q] * 4 + lane];
+      });
+      lds_add(&s.dxacc[(mol * PairPlan13::kN + T.node[sl]) * D + lane], v);
+    });
+  }
+  asm volatile("" ::: "memory");
+}
+
+template <int NF>
+__device__ __forceinline__ void pair_agg(const Lds& s, const f32x16 (&m)[NF], float g, const PairCtx& pc, int lane) {
+  if (pc.tp == 0) pair_agg_tile<0, NF>(s, m, g, pc.mol, pc.sb, lane);
+  else if (pc.tp == 1) pair_agg_tile<1, NF>(s, m, g, pc.mol, pc.sb, lane);
+  else pair_agg_tile<2, NF>(s, m, g, pc.mol, pc.sb, lane);
+}
+
+template <int D>
+__device__ __forceinline__ void pair_shift(const Lds& s, const float (&sh)[D], const PairCtx& pc, int lane) {
+  if (pc.tp == 0) pair_shift_tile<0, D>(s, sh, pc.mol, pc.sb, lane);
+  else if (pc.tp == 1) pair_shift_tile<1, D>(s, sh, pc.mol, pc.sb, lane);
+  else pair_shift_tile<2, D>(s, sh, pc.mol, pc.sb, lane);
+}
+
 // phi_x output Dense(1) (egnn.py:83-85), shifts_ij = phi_x * r_ij / (C + |r_ij|) and their segment sum
 // (egnn.py:87-94)
 template <int NF, int NT, int L, int D>
@@ -1028,6 +1224,115 @@ __device__ __forceinline__ void edge_tail(const Net& net, const BlockW& bw, cons
   phi_x(X, XT);
   edge_shift<NF, NT, L, D>(net, bw, s, X, XT, writer, sc, rr, r, dr, length, dlength, lane, pw);
 }
+
+
+// edge_shift with block-1 pair tiles (pc.sb != nullptr; the M = 128 split primal kernels only, so no other kernel's
+// code changes: a pair context threaded through edge_shift / edge_tail crashed the compiler on the M = 256 strict-fp32
+// tangent vf_kernel, AMDGPU Rewrite AGPR-Copy-MFMA).  phi_x output Dense(1) (egnn.py:83-85), shifts_ij = phi_x * r_ij / (C + |r_ij|) and their segment sum
+// (egnn.py:87-94)
+template <int NF, int NT, int L, int D>
+__device__ __forceinline__ void edge_shift_pc(const Net& net, const BlockW& bw, const Lds& s, const f32x16 (&px)[NF],
+                                           const f32x16 (&pxT)[NF], bool writer, const SegScan& sc, int rr,
+                                           const float (&r)[D], const float (&dr)[D], float length, float dlength,
+                                           int lane, bool pw, const PairCtx& pc) {
+  const int kk = lane >> 5;
+  float phx, phxT;
+  lds_dot<NF, NT>(s.vecs + (2 * L + 1) * (NF * 32), px, pxT, kk, phx, phxT);
+  phx += __shfl_xor(phx, 32);
+  if constexpr (NT) phxT += __shfl_xor(phxT, 32);
+  phx += bw.bx;
+  // full-precision divisions, as the oracle: a reciprocal-multiply form (1 division instead of 2D) moved the DW4
+  // exact-trace PID solves outside their fp32-oracle envelope (tests/test_gpu_eval_modes.py; profiles/round5/dw4_envelope) and
+  // saved no measurable time
+  const float den = net.C + length;
+  const int RP = net.RP;
+  float sh[2 * D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    sh[d] = (phx * r[d]) / den;
+    sh[D + d] = NT ? (phxT * r[d] + phx * dr[d]) / den - (phx * r[d]) * dlength / (den * den) : 0.f;
+  }
+  if (pc.sb) {   // block-1 pair tile: +shift to atom a, -shift to atom b
+    float s3[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) s3[d] = sh[d];
+    pair_shift<D>(s, s3, pc, lane);
+    return;
+  }
+  sc.sum_many<2 * D>(sh);
+  if (writer && kk == 0) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      if (pw) lds_add(&s.dxacc[rr * D + d], sh[d]);
+      if constexpr (NT) lds_add(&s.dxacc[(RP + rr) * D + d], sh[D + d]);
+    }
+  }
+}
+
+// edge_tail with block-1 pair tiles (edge_shift_pc).  Gate, message aggregation, phi_x torso + output, shifts.
+// pw = false: the tile's primal outputs are computed (the tangents need them) but not stored (exact-trace block-1
+// dual tiles, whose edges' primal contributions come from the primal tiles)
+template <int NF, int NT, int L, int D, typename PhiX>
+__device__ __forceinline__ void edge_tail_pc(const Net& net, const BlockW& bw, const Lds& s, f32x16 (&X)[NF],
+                                          f32x16 (&XT)[NF], bool valid, int rr, float* agg_dst,
+                                          const float (&r)[D], const float (&dr)[D], float length, float dlength,
+                                          int lane, bool agg, PhiX&& phi_x, bool pw, const PairCtx& pc) {
+  f32x16(&m)[NF] = X;
+  f32x16(&mT)[NF] = XT;
+  const int kk = lane >> 5, li = lane & 31;
+  SegScan sc;
+  sc.init(valid ? rr : -1, li);
+  const bool writer = valid && sc.tail;
+  const int RP = net.RP;
+  // the gate and the message aggregate only feed phi_h, i.e. h, which the last block's caller never reads (v depends
+  // on x alone, egnn.py:176-188): agg == false skips them (wave-uniform)
+  if (agg) {
+  // gate e_ij = sigmoid(m_ij . w_g + b_g)  (egnn.py:99-101)
+  float part, partT;
+  lds_dot<NF, NT>(s.vecs + (2 * L) * (NF * 32), m, mT, kk, part, partT);
+  part += __shfl_xor(part, 32);
+  if constexpr (NT) partT += __shfl_xor(partT, 32);
+  const float g = sigmoidf_(part + bw.bg);
+  const float gT = NT ? g * (1.0f - g) * partT : 0.f;
+
+  // m_i = scatter_sum(m_ij * e_ij) (the / sqrt(N-1) happens in the node update)   (egnn.py:102-104)
+  if (pc.sb) {   // block-1 pair tile: each pair's m e to both of its atoms
+    pair_agg<NF>(s, m, g, pc, lane);
+  } else {
+#pragma unroll
+  for (int fb = 0; fb < NF; ++fb) {
+    float v[16];
+#pragma unroll
+    for (int r16 = 0; r16 < 16; ++r16) v[r16] = m[fb][r16] * g;
+    sc.sum_many<16>(v);
+    if (writer && pw) {
+      if (agg_dst) {
+        // the segment part's sums as 4 x 16-B stores into its own row (no atomics; combined in the node update)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          *reinterpret_cast<f32x4*>(agg_dst + fb * 32 + 8 * q + 4 * kk) =
+              f32x4{v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
+      } else {
+        agg_rows<NF>(s, rr, kk, fb, v);
+      }
+    }
+    if constexpr (NT) {
+#pragma unroll
+      for (int r16 = 0; r16 < 16; ++r16) v[r16] = gT * m[fb][r16] + g * mT[fb][r16];
+      sc.sum_many<16>(v);
+      if (writer) {
+        agg_rows<NF>(s, RP + rr, kk, fb, v);
+      }
+    }
+  }
+  }  // !pc.sb
+  }  // agg
+
+  // phi_x torso (egnn.py:82) then its Dense(1) and the shifts
+  phi_x(X, XT);
+  edge_shift_pc<NF, NT, L, D>(net, bw, s, X, XT, writer, sc, rr, r, dr, length, dlength, lane, pw, pc);
+}
+
 
 // M = 256 tangent kernels: phi_e.0 on the edge itself, [h_s | h_r | |r|^2] W1 + b1 (egnn.py:76-79; no per-node P
 // halves, whose primal + tangent rows would need 132 KB of LDS), as split MFMAs with the node-GEMM fragment layout
@@ -1244,12 +1549,22 @@ __device__ __forceinline__ void chain_dual_seq_f32(f32x16 (&X)[NF], f32x16 (&XT)
 // dual tiles' primal) for the exact trace's primal-only tiles inside the divergence kernels
 template <int NF, int NT, int L, int D, int P, int WPP = kPieces, bool BN = false>
 __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, const Lds& s, int tile, int lane, bool agg,
-                                          int a = -1, int part = 0, int amode = 1) {
+                                          int a = -1, int part = 0, int amode = 1, float* psb = nullptr) {
   const int kk = lane >> 5, li = lane & 31;
   const int N = net.N, nn1 = N - 1, RP = net.RP, M = NF * 32;
   int mol, i, sd;
   bool valid;
-  if (a < 0) {
+  PairCtx pctx{0, 0, psb};
+  if (psb) {
+    // block-1 pair tile (PairPlan13): tile = 3 molecule + pair tile; lane = pair (a, b), r = x_a - x_b
+    mol = tile / PairPlan13::kTiles;
+    pctx.mol = mol;
+    pctx.tp = tile - PairPlan13::kTiles * mol;
+    const unsigned code = pair13_code(pctx.tp, li);
+    valid = (mol < net.MPW) && code != 0xFFu;
+    i = valid ? (int)(code & 15u) : 0;
+    sd = valid ? (int)(code >> 4) : 1;
+  } else if (a < 0) {
     // each molecule owns EP = 32*ceil(E/32) edge slots, so its tiles (and every rounding inside them) do not
     // depend on which slot of the workgroup, i.e. which batch position, it occupies
     mol = (tile * 32) / net.EP;
@@ -1291,7 +1606,7 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
   // the segment starts, the cross buffer (one row per molecule tile) for its continuation in the next tile
   float* agg_dst = nullptr;
   if constexpr (Geo<NF, NT, P, BN>::kSplit) {
-    if (net.cross) {
+    if (net.cross && !psb) {
       const int tloc = tile - mrow * (net.EP >> 5);
       agg_dst = tloc == ((i * nn1) >> 5) ? s.macc + rr * s.ld_m : s.cross + (mrow * (net.EP >> 5) + tloc) * s.ld_m;
       ECNF_DCHECK(tloc >= 0 && mrow * (net.EP >> 5) + tloc < net.MPW * (net.EP >> 5), 4);
@@ -1331,8 +1646,9 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
     // phi_e layer 1 from the per-node halves: pre = P_s[s] + P_r[r] + |r|^2 w_d  (egnn.py:76,79), SiLU, split
     SplitX<NF> XA, XB;
     f32x16 acc[NF];
-    const float* Ps = s.P + rs * s.ld_P;
-    const float* Pr = s.P + rr * s.ld_P + M;
+    // (pair tiles: the molecule's P row copied to hin before the edge phase; the P rows hold the waves' slices)
+    const float* Ps = psb ? s.hin + mrow * 2 * M : s.P + rs * s.ld_P;
+    const float* Pr = psb ? s.hin + mrow * 2 * M + M : s.P + rr * s.ld_P + M;
     // 4 NF rounds of 4 consecutive features (16-B LDS reads of w_d, P_s, P_r), two rounds per step behind
     // scheduling fences with the next step's reads issued first: the per-round read -> s_waitcnt lgkmcnt(0) ->
     // 2-element SiLU chain form exposed the LDS latency and a wait state after every transcendental
@@ -1374,23 +1690,27 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
     });
     chain_split<NF, L - 1, WPP>(XA, XB, acc, Ws, s.vecs, ie, lane);
     STAMP_LANE0(s, kStEdgeChainE, t_sub);
-    edge_tail<NF, NT, L, D>(net, bw, s, acc, acc, valid, rr, agg_dst, r, dr, length, dlength, lane, agg,
-                            [&](f32x16 (&m)[NF], f32x16 (&)[NF]) {
-                              STAMP_LANE0(s, kStEdgeAgg, t_sub);
-                              // phi_x layers 1..L on the (ungated) messages
-                              static_for<NF>([&](auto Fc) {
-                                constexpr int fb = decltype(Fc)::value;
-                                static_for<8>([&](auto Ic) {
-                                  constexpr int i = decltype(Ic)::value;
-                                  put_pair<NF, fb, 2 * i>(XA, m[fb][2 * i], m[fb][2 * i + 1]);
-                                });
-                              });
-                              const unsigned* Wx = launder_uniform((WPP == 3 ? bw.Ws3 : bw.Ws) +
-                                                                   (size_t)(L - 1) * SplitPlan<NF, 1>::GL * WPP * 256);
-                              STAMP_LANE0(s, kStEdgePhiXIn, t_sub);
-                              chain_split<NF, L, WPP>(XA, XB, m, Wx, s.vecs + (L - 1) * NF * 32, ix, lane);
-                              STAMP_LANE0(s, kStEdgePhiX, t_sub);
-                            });
+    // phi_x layers 1..L on the (ungated) messages
+    auto phi_x = [&](f32x16 (&m)[NF], f32x16 (&)[NF]) {
+      STAMP_LANE0(s, kStEdgeAgg, t_sub);
+      static_for<NF>([&](auto Fc) {
+        constexpr int fb = decltype(Fc)::value;
+        static_for<8>([&](auto Ic) {
+          constexpr int i = decltype(Ic)::value;
+          put_pair<NF, fb, 2 * i>(XA, m[fb][2 * i], m[fb][2 * i + 1]);
+        });
+      });
+      const unsigned* Wx = launder_uniform((WPP == 3 ? bw.Ws3 : bw.Ws) + (size_t)(L - 1) * SplitPlan<NF, 1>::GL * WPP * 256);
+      STAMP_LANE0(s, kStEdgePhiXIn, t_sub);
+      chain_split<NF, L, WPP>(XA, XB, m, Wx, s.vecs + (L - 1) * NF * 32, ix, lane);
+      STAMP_LANE0(s, kStEdgePhiX, t_sub);
+    };
+    // (one call site, the pair tiles branching inside the tail: two, each with its own copy of the phi_x chain, spilled)
+    if constexpr (NT == 0 && NF == 4)
+      edge_tail_pc<NF, NT, L, D>(net, bw, s, acc, acc, valid, rr, agg_dst, r, dr, length, dlength, lane, agg, phi_x,
+                                 true, pctx);
+    else
+      edge_tail<NF, NT, L, D>(net, bw, s, acc, acc, valid, rr, agg_dst, r, dr, length, dlength, lane, agg, phi_x);
     STAMP_LANE0(s, kStEdgeTail, t_sub);
     return;
   }
@@ -1914,7 +2234,8 @@ typedef ECNF_GLOBAL unsigned* gu32_p;
 
 // one exchange of the edge aggregates (MPW = 1; all threads of the workgroup, after the edge phase's barrier)
 template <int NT, int NTHR>
-__device__ __forceinline__ void team_exchange(const Net& net, const Lds& s, const TeamCtx& tm, int epoch) {
+__device__ __forceinline__ void team_exchange(const Net& net, const Lds& s, const TeamCtx& tm, int epoch,
+                                              bool pairs = false) {
   const int G = tm.G;
   if (G <= 1) return;   // a slot that runs alone holds every aggregate already
   const int tid = opaque_tid();
@@ -1932,17 +2253,19 @@ __device__ __forceinline__ void team_exchange(const Net& net, const Lds& s, cons
   auto st16 = [&](int fo, f32x4 v) {   // write-through (sc1) 16-B store of slot float fo
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rsrc, fo * 4, mine, 16);
   };
-  auto first_tile = [&](int i) { return (i * SR) >> 5; };
-  auto last_tile = [&](int i) { return (i * SR + nn1 - 1) >> 5; };
+  // the tiles that hold receiver i's edges (block-1 pair tiles: atom i's pairs, PairPlan13; no continuation rows)
+  auto first_tile = [&](int i) { return pairs ? PairPlan13::tile_lo(i) : (i * SR) >> 5; };
+  auto last_tile = [&](int i) { return pairs ? PairPlan13::tile_hi(i) : (i * SR + nn1 - 1) >> 5; };
+  const bool cross = net.cross && !pairs;
   // ---- publish the rows this member owns
   for (int idx = tid; idx < (1 + NT) * N * M4; idx += NTHR) {
     const int w = idx / (N * M4), iw = idx - w * (N * M4);   // w = 1: the tangent row RP + i
     const int i = iw / M4, c = (iw - i * M4) * 4;
     const bool own = first_tile(i) % G == r ||
-                     (!net.cross && last_tile(i) != first_tile(i) && last_tile(i) % G == r);   // (its second part)
+                     (!cross && last_tile(i) != first_tile(i) && last_tile(i) % G == r);   // (its second part)
     if (own) st16((w * N + i) * M + c, *reinterpret_cast<const f32x4*>(s.macc + (w * RP + i) * s.ld_m + c));
   }
-  if (net.cross)
+  if (cross)
     for (int idx = tid; idx < tpm * M4; idx += NTHR) {
       const int t = idx / M4, c = (idx - t * M4) * 4;
       if (t % G == r) st16(off_x + t * M + c, *reinterpret_cast<const f32x4*>(s.cross + t * s.ld_m + c));
@@ -1991,7 +2314,7 @@ __device__ __forceinline__ void team_exchange(const Net& net, const Lds& s, cons
   // written through by other XCDs' workgroups, so every load is a memory round trip, and one per loop trip
   // serialised ~14 of them per exchange
   constexpr int kB = 8;
-  const int nmsg = (1 + NT) * N * M4, ntot = nmsg + (net.cross ? tpm * M4 : 0);
+  const int nmsg = (1 + NT) * N * M4, ntot = nmsg + (cross ? tpm * M4 : 0);
   for (int base = tid; base < ntot; base += kB * NTHR) {
     f32x4 v[kB];
 #pragma unroll
@@ -2004,7 +2327,7 @@ __device__ __forceinline__ void team_exchange(const Net& net, const Lds& s, cons
         const int o0 = first_tile(i) % G, o1 = last_tile(i) % G;
         v[u] = ld16(o0, (w * N + i) * M + c);
         // atomically accumulated parts (no cross rows): 0 + a + b, whichever member holds each (exact in any order)
-        if (!net.cross && o1 != o0) v[u] += ld16(o1, (w * N + i) * M + c);
+        if (!cross && o1 != o0) v[u] += ld16(o1, (w * N + i) * M + c);
       } else if (idx < ntot) {
         const int t = (idx - nmsg) / M4, c = (idx - nmsg - t * M4) * 4;
         v[u] = ld16(t % G, off_x + t * M + c);
@@ -2045,6 +2368,7 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
   constexpr int kNW = kernel_waves<NF, NT, P, COLS>(), kNT = kernel_threads<NF, NT, P, COLS>();
   constexpr bool kSplitG = Geo<NF, NT, P, BN>::kSplit;
   constexpr bool kSplitN = Geo<NF, NT, P, BN>::kSplitN;   // split node GEMMs (primal split kernels and tangent kernels)
+  constexpr bool kPairs = kSplitG && NF == 4 && !COLS;    // block-1 pair tiles compiled (Net::pairs turns them on)
   // the exact trace's sparse blocks (primal + dual tiles, see the edge loop) in the M <= 128 split tangent kernels;
   // not compiled for the L = 2 shapes (M, D) = (128, 3), (64, 2), where the primal tile's code beside the dual
   // tile's spilled 36 B per lane (tests/test_kernel_resources.py).  The BASELINE shapes (LJ13 128/3/3, ALDP 64/2/3,
@@ -2131,6 +2455,21 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
                                         lane);
       __syncthreads();
     }
+    // block-1 pair tiles: every atom of a molecule has the same P row; copy one per molecule to hin (dead until the
+    // node update) so the P rows can hold the waves' transposition slices, and restart macc from +0 (the pairs'
+    // aggregates are atomic, the receiver segments' first parts were stores)
+    const bool pairs = kPairs && k == 0 && net.pairs;
+    if (pairs) {
+      for (int idx = tid; idx < MPW * 2 * M; idx += kNT) {
+        const int m = idx / (2 * M), c = idx - m * (2 * M);
+        s.hin[idx] = s.P[m * N * s.ld_P + c];
+      }
+      for (int idx = tid; idx < RP * M; idx += kNT) {
+        const int row = idx / M, c = idx - row * M;
+        s.macc[row * s.ld_m + c] = 0.f;
+      }
+      __syncthreads();
+    }
     STAMP(s, kStPGemm);
     // edges
     // tile t runs on wave t mod NW, i.e. SIMD t mod 4: every SIMD gets ceil/floor(ntiles / 4) tiles
@@ -2183,7 +2522,9 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
         }
       }
       const int nd = nact * ndt;
-      const int nrun = nd + (pload ? 0 : nact * tpm);
+      const int tpb = pairs ? PairPlan13::kTiles : tpm;   // this block's tiles per molecule
+      float* psb = pairs ? s.P + wave * 1024 : nullptr;
+      const int nrun = nd + (pload ? 0 : nact * tpb);
       // team mode (MPW = 1): this member runs tiles t = r, r + G, ... of the molecule (team_exchange)
       const int tstep = TEAM ? tm->G : 1, tfirst = TEAM ? tm->r : 0;
       if constexpr (COLS) {
@@ -2202,22 +2543,24 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
             continue;
           }
         }
-        const int v2 = vt - nd, q = v2 / tpm;
-        const int tile = nth_active(q) * tpm + (v2 - q * tpm);
+        const int v2 = vt - nd, q = v2 / tpb;
+        const int tile = nth_active(q) * tpb + (v2 - q * tpb);
         if constexpr (kSparseX) {
           if (ndt) {
             edge_tile<NF, 0, L, D, P, 3>(net, bw, s, tile, elane, need_h);   // exact weights, as the dual tiles
             continue;
           }
         }
-        edge_tile<NF, NT, L, D, P, kPieces, BN>(net, bw, s, tile, elane, need_h);
+        // (one call site: the pair tiles branch inside the tile around one copy of its chains; a second inlined copy
+        // for block 1 grew the kernel by 40 KB of code and ran 6.7x slower)
+        edge_tile<NF, NT, L, D, P, kPieces, BN>(net, bw, s, tile, elane, need_h, -1, 0, 1, psb);
       }
       }   // !COLS
     }
     __syncthreads();
     if constexpr (TEAM) {   // team mode: rebuild the molecule's aggregates from every member's tiles
       STAMP(s, kStEdge);
-      team_exchange<NT, kNT>(net, s, *tm, *tepoch);
+      team_exchange<NT, kNT>(net, s, *tm, *tepoch, pairs);
       ++*tepoch;
       STAMP(s, kStTeam);
     }
@@ -2254,7 +2597,7 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
       // the split phi_h.0 weights carry the message scale -ln2 / sqrt(N-1) (log2-domain messages, chain_split.hpp;
       // egnn.py:104), so only the continuation parts of the segments that cross a tile boundary are added here:
       // one (molecule, crossing) row per wave trip, wave-uniform indices
-      if (net.cross) {
+      if (net.cross && !pairs) {
         const int nx = net.ncross, tpm = net.EP >> 5;
         for (int j = wave; j < MPW * nx; j += kNW) {
           const int m = j / nx, q = j - m * nx;
@@ -2271,7 +2614,7 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
     }
     __syncthreads();
     if constexpr (kSplitG) {
-      if (net.cross) {   // the cross buffer overlaid hin's time-embedding columns: restore them
+      if (net.cross || pairs) {   // the cross buffer (pair tiles: the P copies) overlaid hin's time-embedding columns
         for (int idx = tid; idx < nvalid * T; idx += kNT) {
           const int row = idx / T, c = idx - row * T;
           s.hin[row * s.ld_hin + H + c] = s.temb[(row / N) * T + c];
