@@ -67,6 +67,24 @@ def live_flops_per_eval(cfg) -> float:
     return flops_per_eval(cfg) - dead_flops_per_eval(cfg)
 
 
+def pair_tiles_active(cfg, chain_mode: str) -> bool:
+    """Block-1 pair tiles (egnn_eval.hpp PairPlan13; set in ecnf_hip.hip ecnf_create): one node feature, 13 atoms,
+    the M = 128 split primal kernels."""
+    return chain_mode in SPLIT_TERMS and cfg.n_features == 1 and cfg.n_nodes == 13 and cfg.mlp_width == 128
+
+
+def executed_flops_per_eval(cfg, chain_mode: str) -> float:
+    """live_flops_per_eval as the kernel executes it: with pair tiles, block 1's edge work (layer-1 assembly, the phi_e
+    and phi_x chains, the gate and phi_x-output dots) runs once per unordered pair, half the edges (m_ij = m_ji there)."""
+    F = live_flops_per_eval(cfg)
+    if not pair_tiles_active(cfg, chain_mode):
+        return F
+    N, M, L = cfg.n_nodes, cfg.mlp_width, cfg.mlp_depth
+    E = N * (N - 1)
+    edge_block = 3 * E * M + 2 * E * (L - 1) * M * M + 2 * E * L * M * M + 4 * E * M
+    return F - edge_block / 2
+
+
 def vector_flops_per_eval(cfg) -> float:
     """The part of live_flops_per_eval that is not a GEMM (runs on the fp32 VALU): phi_e layer-1 assembly (3EM), the
     phi_x-output dot product (2EM) and the gate dot product (2EM, every block but the last)."""
@@ -400,6 +418,7 @@ def main():
     achieved = F * nfe_seen * B / (kernel_ms * 1e-3) / 1e12
     chain_mode = h.chain_arithmetic()
     peak = roofline_peak(cfg, chain_mode)
+    Fx = executed_flops_per_eval(cfg, chain_mode)
 
     # the strict-fp32 kernels (every GEMM on v_mfma_f32_32x32x2_f32) on the same workload, for comparison
     fp32 = None
@@ -592,6 +611,10 @@ def main():
                          "flop_per_launch": F * nfe_seen * B,
                          "flop_basis": "live dense-contraction FLOPs per EGNN eval (SURVEY 8d F minus the last "
                                        "block's dead h update) x NFE x batch",
+                         # the FLOPs the kernel executes (block-1 pair tiles skip the mirrored half of block 1's edge
+                         # work) and the fraction of the same ceiling they reach
+                         "flop_executed_per_launch": Fx * nfe_seen * B,
+                         "frac_executed": achieved * (Fx / F) / peak,
                          "frac_vs_fp32_mfma_peak": achieved / PEAK_FP32_MFMA_TFLOPS,
                          "pmc": pmc,
                          "frac_at_grbm_clock": (achieved / (peak * pmc["clock_ghz_grbm"] / 2.4)
