@@ -1211,9 +1211,11 @@ int ecnf_create(const ecnf_cfg* cfg, const float* params, size_t n_floats, int d
       n.lds_floats = (int)(lds / 4);
       h->lds[ix] = lds;
       // block-1 pair tiles (egnn_eval.hpp PairPlan13): one node feature (every atom's block-1 h is the same), 13 atoms,
-      // the M = 128 split primal kernels (8 waves, each with a 1024-float slice of the >= 32 x 260-float P rows)
-      n.pairs = (NT == 0 && P == 0 && split_primal(c, 0, 0) && c.n_features == 1 && c.n_nodes == 13 &&
-                 c.mlp_width == 128 && primal_waves(c) * 1024 <= 32 * 260) ? 1 : 0;
+      // the M = 128 split primal kernels (8 waves, each with a 1024-float slice of the >= 32 x 260-float P rows) and
+      // split tangent kernels (4 waves; 64 P rows)
+      n.pairs = (P == 0 && c.n_features == 1 && c.n_nodes == 13 && c.mlp_width == 128 &&
+                 (NT == 0 ? split_primal(c, 0, 0) && primal_waves(c) * 1024 <= 32 * 260 : !wide_tangent(c, 1, 0)))
+                    ? 1 : 0;
     } else {
       n.MPW = 0;
       h->lds[ix] = 0;

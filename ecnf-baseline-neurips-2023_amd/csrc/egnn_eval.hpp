@@ -1065,17 +1065,18 @@ struct PairCtx {
   int mol;     // molecule slot in the workgroup
   int tp;      // pair tile of the molecule (0 .. 2)
   float* sb;   // this wave's 1024-float transposition slice (16-B aligned)
+  int rp;      // tangent row offset RP (the divergence kernels' tangent aggregates and shifts)
 };
 
 // m_i += sum over atom i's pairs of m e (egnn.py:102-104) for pair tile TP: per pass two 32-feature blocks, the tile's
 // pairs in two halves of 16 LDS rows of 64 features (16-B chunks XOR-swizzled by row: conflict-free column reads), then
 // lane c sums feature c over each atom's pairs (fixed order) and adds it to macc
-template <int TP, int NF>
-__device__ __forceinline__ void pair_agg_tile(const Lds& s, const f32x16 (&m)[NF], float g, int mol, float* sb,
-                                              int lane) {
+// (val(fb, r): the value of accumulator register r of block fb; row0: 0, or RP for the tangent aggregates)
+template <int TP, int NF, typename Val>
+__device__ __forceinline__ void pair_agg_tile(const Lds& s, Val&& val, int mol, int row0, float* sb, int lane) {
   constexpr PairPlan13::Tile T = PairPlan13::make(TP);
   const int kk = lane >> 5, li = lane & 31, ch = lane >> 2, e = lane & 3;
-  float* mrows = s.macc + mol * PairPlan13::kN * s.ld_m + lane;
+  float* mrows = s.macc + (row0 + mol * PairPlan13::kN) * s.ld_m + lane;
   static_for<NF / 2>([&](auto Pc) {
     constexpr int pass = decltype(Pc)::value;
     float acc[T.nn];
@@ -1089,7 +1090,7 @@ __device__ __forceinline__ void pair_agg_tile(const Lds& s, const f32x16 (&m)[NF
             constexpr int q = decltype(Qc)::value;
             const int c16 = fbl * 8 + 2 * q + kk;   // features 8q + 4kk .. +3 of block fb (accumulator rows 4q .. 4q+3)
             *reinterpret_cast<f32x4*>(sb + p * 64 + ((c16 ^ p) << 2)) =
-                f32x4{m[fb][4 * q] * g, m[fb][4 * q + 1] * g, m[fb][4 * q + 2] * g, m[fb][4 * q + 3] * g};
+                f32x4{val(fb, 4 * q), val(fb, 4 * q + 1), val(fb, 4 * q + 2), val(fb, 4 * q + 3)};
           });
         });
       }
@@ -1121,50 +1122,64 @@ __device__ __forceinline__ void pair_agg_tile(const Lds& s, const f32x16 (&m)[NF
   });
 }
 
-// shift_i += sum over atom i's pairs of +-phi_x r / (C + |r|) (egnn.py:87-94) for pair tile TP: rows of 8 floats
-// [+shift | -shift], lanes d < D sum each atom's pairs (fixed order)
-template <int TP, int D>
-__device__ __forceinline__ void pair_shift_tile(const Lds& s, const float (&sh)[D], int mol, float* sb, int lane) {
-  static_assert(D <= 4, "one 16-B half row per sign");
+// shift_i += sum over atom i's pairs of +-phi_x r / (C + |r|) (egnn.py:87-94) for pair tile TP, and the tangent shifts
+// (V = D or 2 D values per pair: the tangent of shift_ji = -shift_ij is -dshift_ij): rows of 16 floats [+v | -v],
+// lanes d < V sum each atom's pairs (fixed order) into dxacc (tangent values into the rows RP + n)
+template <int TP, int V, int D>
+__device__ __forceinline__ void pair_shift_tile(const Lds& s, const float (&sh)[V], int mol, int rp, float* sb, int lane) {
+  static_assert(V <= 8 && (V == D || V == 2 * D), "primal, or primal + tangent shifts");
   constexpr PairPlan13::Tile T = PairPlan13::make(TP);
   const int kk = lane >> 5, li = lane & 31;
   if (kk == 0) {
-    f32x4 pv = {0.f, 0.f, 0.f, 0.f}, nv = {0.f, 0.f, 0.f, 0.f};
+    f32x4 pv[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}}, nv[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
-    for (int d = 0; d < D; ++d) {
-      pv[d] = sh[d];
-      nv[d] = -sh[d];
+    for (int d = 0; d < V; ++d) {
+      pv[d >> 2][d & 3] = sh[d];
+      nv[d >> 2][d & 3] = -sh[d];
     }
-    *reinterpret_cast<f32x4*>(sb + li * 8) = pv;
-    *reinterpret_cast<f32x4*>(sb + li * 8 + 4) = nv;
+    static_for<(V + 3) / 4>([&](auto Hc) {
+      constexpr int hh = decltype(Hc)::value;
+      *reinterpret_cast<f32x4*>(sb + li * 16 + 4 * hh) = pv[hh];
+      *reinterpret_cast<f32x4*>(sb + li * 16 + 8 + 4 * hh) = nv[hh];
+    });
   }
   asm volatile("" ::: "memory");
-  if (lane < D) {
+  if (lane < V) {
+    const int row = lane < D ? mol * PairPlan13::kN : rp + mol * PairPlan13::kN, d = lane < D ? lane : lane - D;
     static_for<T.nn>([&](auto Sc) {
       constexpr int sl = decltype(Sc)::value;
       float v = 0.f;
       static_for<T.deg[sl]>([&](auto Qc) {
         constexpr int q = decltype(Qc)::value;
-        v += sb[T.lane[sl][q] * 8 + T.role[sl][q] * 4 + lane];
+        v += sb[T.lane[sl][q] * 16 + T.role[sl][q] * 8 + lane];
       });
-      lds_add(&s.dxacc[(mol * PairPlan13::kN + T.node[sl]) * D + lane], v);
+      lds_add(&s.dxacc[(row + T.node[sl]) * D + d], v);
     });
   }
   asm volatile("" ::: "memory");
 }
 
-template <int NF>
-__device__ __forceinline__ void pair_agg(const Lds& s, const f32x16 (&m)[NF], float g, const PairCtx& pc, int lane) {
-  if (pc.tp == 0) pair_agg_tile<0, NF>(s, m, g, pc.mol, pc.sb, lane);
-  else if (pc.tp == 1) pair_agg_tile<1, NF>(s, m, g, pc.mol, pc.sb, lane);
-  else pair_agg_tile<2, NF>(s, m, g, pc.mol, pc.sb, lane);
+// m e to both atoms of each pair (primal rows), and for NT = 1 its tangent gT m + g mT (rows RP + n)
+template <int NF, int NT>
+__device__ __forceinline__ void pair_agg(const Lds& s, const f32x16 (&m)[NF], const f32x16 (&mT)[NF], float g, float gT,
+                                         const PairCtx& pc, int lane) {
+  auto prim = [&](int fb, int r) { return m[fb][r] * g; };
+  auto tang = [&](int fb, int r) { return gT * m[fb][r] + g * mT[fb][r]; };
+  auto one = [&](auto Tc) {
+    constexpr int TP = decltype(Tc)::value;
+    pair_agg_tile<TP, NF>(s, prim, pc.mol, 0, pc.sb, lane);
+    if constexpr (NT) pair_agg_tile<TP, NF>(s, tang, pc.mol, pc.rp, pc.sb, lane);
+  };
+  if (pc.tp == 0) one(std::integral_constant<int, 0>{});
+  else if (pc.tp == 1) one(std::integral_constant<int, 1>{});
+  else one(std::integral_constant<int, 2>{});
 }
 
-template <int D>
-__device__ __forceinline__ void pair_shift(const Lds& s, const float (&sh)[D], const PairCtx& pc, int lane) {
-  if (pc.tp == 0) pair_shift_tile<0, D>(s, sh, pc.mol, pc.sb, lane);
-  else if (pc.tp == 1) pair_shift_tile<1, D>(s, sh, pc.mol, pc.sb, lane);
-  else pair_shift_tile<2, D>(s, sh, pc.mol, pc.sb, lane);
+template <int V, int D>
+__device__ __forceinline__ void pair_shift(const Lds& s, const float (&sh)[V], const PairCtx& pc, int lane) {
+  if (pc.tp == 0) pair_shift_tile<0, V, D>(s, sh, pc.mol, pc.rp, pc.sb, lane);
+  else if (pc.tp == 1) pair_shift_tile<1, V, D>(s, sh, pc.mol, pc.rp, pc.sb, lane);
+  else pair_shift_tile<2, V, D>(s, sh, pc.mol, pc.rp, pc.sb, lane);
 }
 
 // phi_x output Dense(1) (egnn.py:83-85), shifts_ij = phi_x * r_ij / (C + |r_ij|) and their segment sum
@@ -1288,11 +1303,11 @@ __device__ __forceinline__ void edge_shift_pc(const Net& net, const BlockW& bw, 
     sh[d] = (phx * r[d]) / den;
     sh[D + d] = NT ? (phxT * r[d] + phx * dr[d]) / den - (phx * r[d]) * dlength / (den * den) : 0.f;
   }
-  if (pc.sb) {   // block-1 pair tile: +shift to atom a, -shift to atom b
-    float s3[D];
+  if (pc.sb) {   // block-1 pair tile: +shift (and its tangent) to atom a, -shift to atom b
+    float sv[(1 + NT) * D];
 #pragma unroll
-    for (int d = 0; d < D; ++d) s3[d] = sh[d];
-    pair_shift<D>(s, s3, pc, lane);
+    for (int d = 0; d < (1 + NT) * D; ++d) sv[d] = sh[d];
+    pair_shift<(1 + NT) * D, D>(s, sv, pc, lane);
     return;
   }
   sc.sum_many<2 * D>(sh);
@@ -1333,7 +1348,7 @@ __device__ __forceinline__ void edge_tail_pc(const Net& net, const BlockW& bw, c
 
   // m_i = scatter_sum(m_ij * e_ij) (the / sqrt(N-1) happens in the node update)   (egnn.py:102-104)
   if (pc.sb) {   // block-1 pair tile: each pair's m e to both of its atoms
-    pair_agg<NF>(s, m, g, pc, lane);
+    pair_agg<NF, NT>(s, m, mT, g, gT, pc, lane);
   } else {
 #pragma unroll
   for (int fb = 0; fb < NF; ++fb) {
@@ -1590,7 +1605,7 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
   const int N = net.N, nn1 = N - 1, RP = net.RP, M = NF * 32;
   int mol, i, sd;
   bool valid;
-  PairCtx pctx{0, 0, psb};
+  PairCtx pctx{0, 0, psb, net.RP};
   if (psb) {
     // block-1 pair tile (PairPlan13): tile = 3 molecule + pair tile; lane = pair (a, b), r = x_a - x_b
     mol = tile / PairPlan13::kTiles;
@@ -1756,10 +1771,13 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
     constexpr float kNegLn2 = -0.69314718055994531f;
     SplitX<NF> XA, XB, XAT, XBT;
     f32x16 X[NF], XT[NF];
-    const float* Ps = s.P + rs * s.ld_P;
-    const float* Pr = s.P + rr * s.ld_P + M;
-    const float* PsT = s.P + (RP + rs) * s.ld_P;
-    const float* PrT = s.P + (RP + rr) * s.ld_P + M;
+    // (pair tiles: the molecule's primal and tangent P rows copied to hin, as the primal kernels')
+    const float* pcp = s.hin + mrow * 2 * M;
+    const float* pct = s.hin + (net.MPW + mrow) * 2 * M;
+    const float* Ps = psb ? pcp : s.P + rs * s.ld_P;
+    const float* Pr = psb ? pcp + M : s.P + rr * s.ld_P + M;
+    const float* PsT = psb ? pct : s.P + (RP + rs) * s.ld_P;
+    const float* PrT = psb ? pct + M : s.P + (RP + rr) * s.ld_P + M;
     // as the primal split kernels: one round of 4 features per fenced step, the next round's 5 reads issued first
     constexpr int NQ = 4 * NF;
     auto rd5 = [&](int q, f32x4 (&o)[5]) {
@@ -1804,25 +1822,27 @@ __device__ __forceinline__ void edge_tile(const Net& net, const BlockW& bw, cons
     STAMP_LANE0(s, kStEdgeChainE, t_sub);
     // the tail stays in the log2 domain as in the primal split kernels: gate / shift with the -ln2-folded w_g', w_x'
     // (staged in vecs), the aggregate's -ln2 / sqrt(N-1) in the split phi_h.0 weights, phi_x fed the messages as is
-    edge_tail<NF, NT, L, D>(net, bw, s, X, XT, valid, rr, agg_dst, r, dr, length, dlength, lane, agg,
-                            [&](f32x16 (&Y)[NF], f32x16 (&YT)[NF]) {
-                              STAMP_LANE0(s, kStEdgeAgg, t_sub);
-                              const unsigned* Wx =
-                                  launder_uniform(bw.Ws3 + (size_t)(L - 1) * SplitPlan<NF, 1>::GL * 3 * 256);
-                              static_for<NF>([&](auto Fc) {
-                                constexpr int fb = decltype(Fc)::value;
-                                static_for<8>([&](auto Ic) {
-                                  constexpr int i = decltype(Ic)::value;
-                                  put_pair<NF, fb, 2 * i>(XA, Y[fb][2 * i], Y[fb][2 * i + 1]);
-                                  put_pair<NF, fb, 2 * i>(XAT, YT[fb][2 * i], YT[fb][2 * i + 1]);
-                                });
-                              });
-                              STAMP_LANE0(s, kStEdgePhiXIn, t_sub);
-                              chain_split<NF, L, 1, 3>(XA, XB, Y, Wx, s.vecs + (L - 1) * NF * 32, ix, lane, XAT, XBT,
-                                                       YT);
-                              STAMP_LANE0(s, kStEdgePhiX, t_sub);
-                            },
-                            a < 0);   // block-1 dual tiles of the exact trace store tangents only
+    auto phi_x = [&](f32x16 (&Y)[NF], f32x16 (&YT)[NF]) {
+      STAMP_LANE0(s, kStEdgeAgg, t_sub);
+      const unsigned* Wx = launder_uniform(bw.Ws3 + (size_t)(L - 1) * SplitPlan<NF, 1>::GL * 3 * 256);
+      static_for<NF>([&](auto Fc) {
+        constexpr int fb = decltype(Fc)::value;
+        static_for<8>([&](auto Ic) {
+          constexpr int i = decltype(Ic)::value;
+          put_pair<NF, fb, 2 * i>(XA, Y[fb][2 * i], Y[fb][2 * i + 1]);
+          put_pair<NF, fb, 2 * i>(XAT, YT[fb][2 * i], YT[fb][2 * i + 1]);
+        });
+      });
+      STAMP_LANE0(s, kStEdgePhiXIn, t_sub);
+      chain_split<NF, L, 1, 3>(XA, XB, Y, Wx, s.vecs + (L - 1) * NF * 32, ix, lane, XAT, XBT, YT);
+      STAMP_LANE0(s, kStEdgePhiX, t_sub);
+    };
+    // (a < 0: block-1 dual tiles of the exact trace store tangents only)
+    if constexpr (NF == 4)
+      edge_tail_pc<NF, NT, L, D>(net, bw, s, X, XT, valid, rr, agg_dst, r, dr, length, dlength, lane, agg, phi_x,
+                                 a < 0, pctx);
+    else
+      edge_tail<NF, NT, L, D>(net, bw, s, X, XT, valid, rr, agg_dst, r, dr, length, dlength, lane, agg, phi_x, a < 0);
     STAMP_LANE0(s, kStEdgeTail, t_sub);
     return;
   }
@@ -2404,7 +2424,8 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
   constexpr int kNW = kernel_waves<NF, NT, P, COLS>(), kNT = kernel_threads<NF, NT, P, COLS>();
   constexpr bool kSplitG = Geo<NF, NT, P, BN>::kSplit;
   constexpr bool kSplitN = Geo<NF, NT, P, BN>::kSplitN;   // split node GEMMs (primal split kernels and tangent kernels)
-  constexpr bool kPairs = kSplitG && NF == 4 && !COLS;    // block-1 pair tiles compiled (Net::pairs turns them on)
+  // block-1 pair tiles compiled (Net::pairs turns them on): the M = 128 split primal and split tangent kernels
+  constexpr bool kPairs = (kSplitG || Geo<NF, NT, P, BN>::kL2T) && NF == 4 && !COLS;
   // the exact trace's sparse blocks (primal + dual tiles, see the edge loop) in the M <= 128 split tangent kernels;
   // not compiled for the L = 2 shapes (M, D) = (128, 3), (64, 2), where the primal tile's code beside the dual
   // tile's spilled 36 B per lane (tests/test_kernel_resources.py).  The BASELINE shapes (LJ13 128/3/3, ALDP 64/2/3,
@@ -2494,13 +2515,14 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
     // block-1 pair tiles: every atom of a molecule has the same P row; copy one per molecule to hin (dead until the
     // node update) so the P rows can hold the waves' transposition slices, and restart macc from +0 (the pairs'
     // aggregates are atomic, the receiver segments' first parts were stores)
-    const bool pairs = kPairs && k == 0 && net.pairs;
+    // (not in the exact trace, whose block 1 runs dual tiles at one atom)
+    const bool pairs = kPairs && k == 0 && net.pairs && sparse_a < 0;
     if (pairs) {
-      for (int idx = tid; idx < MPW * 2 * M; idx += kNT) {
-        const int m = idx / (2 * M), c = idx - m * (2 * M);
-        s.hin[idx] = s.P[m * N * s.ld_P + c];
+      for (int idx = tid; idx < (1 + NT) * MPW * 2 * M; idx += kNT) {   // primal rows, then the tangent rows
+        const int w = idx / (MPW * 2 * M), m = (idx - w * MPW * 2 * M) / (2 * M), c = idx % (2 * M);
+        s.hin[idx] = s.P[(w * RP + m * N) * s.ld_P + c];
       }
-      for (int idx = tid; idx < RP * M; idx += kNT) {
+      for (int idx = tid; idx < R * M; idx += kNT) {
         const int row = idx / M, c = idx - row * M;
         s.macc[row * s.ld_m + c] = 0.f;
       }
@@ -2649,7 +2671,7 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
       }
     }
     __syncthreads();
-    if constexpr (kSplitG) {
+    if constexpr (kSplitG || kPairs) {
       if (net.cross || pairs) {   // the cross buffer (pair tiles: the P copies) overlaid hin's time-embedding columns
         for (int idx = tid; idx < nvalid * T; idx += kNT) {
           const int row = idx / T, c = idx - row * T;

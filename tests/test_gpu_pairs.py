@@ -91,3 +91,23 @@ def test_pair_tiles_deterministic_and_batch_independent(handles):
     va = h1.vector_field(x, t, feat)
     vs = h1.vector_field(x[5:9].contiguous(), t[5:9].contiguous(), feat[5:9].contiguous())
     assert torch.equal(vs, va[5:9])
+
+
+@pytest.mark.timeout(120)
+def test_pair_tiles_tangents_match_segment_path(handles):
+    """The divergence kernels' pair tiles (the tangent of a pair's message is symmetric too, its shift's tangent
+    antisymmetric): JVPs and a Hutchinson log-density against the two-feature (segment-path) network."""
+    cfg, _, _, h1, h2 = handles
+    B = 64
+    z, t, feat = _inputs(cfg, B, 13)
+    x = h1.base_sample(z)
+    u = torch.randn((B, 2, cfg.event_dim), device=DEV, generator=torch.Generator("cuda").manual_seed(14))
+    v1, j1 = h1.jvp(x, t, feat, u)
+    v2, j2 = h2.jvp(x, t, feat, u)
+    assert float((v1 - v2).abs().max()) <= 2e-6 * max(1.0, float(v2.abs().max()))
+    assert float((j1 - j2).abs().max()) <= 2e-6 * max(1.0, float(j2.abs().max()))
+    o = SolveOptions("euler", 0.05)
+    y1, d1 = h1.integrate(x, feat, 1.0, 0.0, o, _lib.DIV_HUTCHINSON, z)[:2]
+    y2, d2 = h2.integrate(x, feat, 1.0, 0.0, o, _lib.DIV_HUTCHINSON, z)[:2]
+    assert float((y1 - y2).abs().max()) <= 2e-5 * max(1.0, float(y2.abs().max()))
+    assert float((d1 - d2).abs().max()) <= 2e-5 * max(1.0, float(d2.abs().max()))
