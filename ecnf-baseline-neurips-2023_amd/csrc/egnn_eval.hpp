@@ -1018,7 +1018,7 @@ constexpr bool pair_plan13_valid() {
   int tiles_of[13] = {};
   for (int t = 0; t < PairPlan13::kTiles; ++t) {
     const PairPlan13::Tile x = PairPlan13::make(t);
-    if (x.np > 32 || x.nn > PairPlan13::kMaxNodes) return false;
+    if (x.np > 30 || x.nn > PairPlan13::kMaxNodes) return false;   // (two halves of 15 transposition rows)
     for (int p = 0; p < x.np; ++p) {
       if (!(x.a[p] < x.b[p] && x.b[p] < 13)) return false;
       ++seen[x.a[p]][x.b[p]];
@@ -1069,27 +1069,29 @@ struct PairCtx {
 };
 
 // m_i += sum over atom i's pairs of m e (egnn.py:102-104) for pair tile TP: per pass two 32-feature blocks, the tile's
-// pairs in two halves of 16 LDS rows of 64 features (16-B chunks XOR-swizzled by row: conflict-free column reads), then
-// lane c sums feature c over each atom's pairs (fixed order) and adds it to macc
+// pairs in two halves of 15 LDS rows of 64 features (+4 padding), then lane c sums feature c over each atom's pairs
+// (fixed order) and adds it to macc
 // (val(fb, r): the value of accumulator register r of block fb; row0: 0, or RP for the tangent aggregates)
 template <int TP, int NF, typename Val>
 __device__ __forceinline__ void pair_agg_tile(const Lds& s, Val&& val, int mol, int row0, float* sb, int lane) {
   constexpr PairPlan13::Tile T = PairPlan13::make(TP);
-  const int kk = lane >> 5, li = lane & 31, ch = lane >> 2, e = lane & 3;
+  const int kk = lane >> 5, li = lane & 31;
   float* mrows = s.macc + (row0 + mol * PairPlan13::kN) * s.ld_m + lane;
   static_for<NF / 2>([&](auto Pc) {
     constexpr int pass = decltype(Pc)::value;
     float acc[T.nn];
     static_for<2>([&](auto Hc) {
       constexpr int h = decltype(Hc)::value;
-      if ((li >> 4) == h) {
-        const int p = li & 15;
+      // this half's pairs (15: 1020 floats) as rows of 68 floats (16-B chunks; 4-bank row shift: conflict-free column
+      // reads at immediate offsets.  An XOR-swizzled 64-float form needed 2-3 address VALU per read and 32 more registers)
+      if (li >= 15 * h && li < 15 * h + 15) {
+        const int p = li - 15 * h;
         static_for<2>([&](auto Fc) {
           constexpr int fbl = decltype(Fc)::value, fb = 2 * pass + fbl;
           static_for<4>([&](auto Qc) {
             constexpr int q = decltype(Qc)::value;
-            const int c16 = fbl * 8 + 2 * q + kk;   // features 8q + 4kk .. +3 of block fb (accumulator rows 4q .. 4q+3)
-            *reinterpret_cast<f32x4*>(sb + p * 64 + ((c16 ^ p) << 2)) =
+            const int c16 = fbl * 8 + 2 * q + kk;
+            *reinterpret_cast<f32x4*>(sb + p * 68 + (c16 << 2)) =
                 f32x4{val(fb, 4 * q), val(fb, 4 * q + 1), val(fb, 4 * q + 2), val(fb, 4 * q + 3)};
           });
         });
@@ -1106,7 +1108,7 @@ __device__ __forceinline__ void pair_agg_tile(const Lds& s, Val&& val, int mol, 
         else v = acc[sl];
         static_for<T.deg[sl]>([&](auto Qc) {
           constexpr int p = T.lane[sl][decltype(Qc)::value];
-          if constexpr ((p >> 4) == h) v += sb[(p & 15) * 64 + ((ch ^ (p & 15)) << 2) + e];
+          if constexpr (p / 15 == h) v += sb[(p - 15 * h) * 68 + lane];
         });
         acc[sl] = v;
 #if ECNF_PAIR_NODE_FENCE
