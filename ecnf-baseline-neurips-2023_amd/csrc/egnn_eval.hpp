@@ -2506,20 +2506,42 @@ __device__ __forceinline__ void egnn_eval(const Net& net, const Lds& s, const fl
                                       false, nullptr, 0, s.hb, s.ld_hb, RP, nvalid, wave, lane);
     __syncthreads();
     STAMP(s, kStNodeDense);
+    // block-1 pair tiles (not in the exact trace, whose block 1 runs dual tiles at one atom): every atom of a molecule
+    // has the same P row, held per molecule in hin (dead until the node update) so that the P rows can hold the waves'
+    // transposition slices; macc restarts from +0 (the pairs' aggregates are atomic, the receiver segments' first parts
+    // were stores)
+    const bool pairs = kPairs && k == 0 && net.pairs && sparse_a < 0;
     // per-node halves of phi_e layer 1 (the M = 256 tangent kernels compute layer 1 per edge)
+    bool pcopied = false;
     if constexpr (!Geo<NF, NT, P, BN>::kNoP) {
       constexpr bool kPu = kSplitG || Geo<NF, NT, P, BN>::kL2T;   // log2-domain P
-      node_gemm<NT, kNW, kSplitN, Geo<NF, NT, P, BN>::kNodePFA>(s.hb, s.ld_hb, H, nullptr, 0, 0, bw.Wp, bw.Wp_s, bw.pinv, 2 * M,
-                                        kPu ? bw.bp_u : bw.bp, 2 * M, false, nullptr, 0, s.P, s.ld_P, RP, nvalid, wave,
-                                        lane);
-      __syncthreads();
+      if (NT == 0 && pairs) {
+        // primal pair blocks: P for one row per molecule only, as one 32-row tile (its rows past MPW read whatever
+        // follows and are not stored): the molecules' hb rows gathered behind the P copies, the P GEMM writing the
+        // copies directly.  Each P row is the same MFMA sequence as in the full GEMM (bitwise), on half the tasks
+        float* hbc = s.hin + MPW * 2 * M;
+        for (int idx = tid; idx < MPW * H; idx += kNT) {
+          const int m = idx / H, c = idx - m * H;
+          hbc[m * s.ld_hb + c] = s.hb[m * N * s.ld_hb + c];
+        }
+        for (int idx = tid; idx < R * M; idx += kNT) {
+          const int row = idx / M, c = idx - row * M;
+          s.macc[row * s.ld_m + c] = 0.f;
+        }
+        __syncthreads();
+        node_gemm<NT, kNW, kSplitN, Geo<NF, NT, P, BN>::kNodePFA>(hbc, s.ld_hb, H, nullptr, 0, 0, bw.Wp, bw.Wp_s, bw.pinv,
+                                          2 * M, kPu ? bw.bp_u : bw.bp, 2 * M, false, nullptr, 0, s.hin, 2 * M, 32, MPW,
+                                          wave, lane);
+        __syncthreads();
+        pcopied = true;
+      } else {
+        node_gemm<NT, kNW, kSplitN, Geo<NF, NT, P, BN>::kNodePFA>(s.hb, s.ld_hb, H, nullptr, 0, 0, bw.Wp, bw.Wp_s, bw.pinv, 2 * M,
+                                          kPu ? bw.bp_u : bw.bp, 2 * M, false, nullptr, 0, s.P, s.ld_P, RP, nvalid, wave,
+                                          lane);
+        __syncthreads();
+      }
     }
-    // block-1 pair tiles: every atom of a molecule has the same P row; copy one per molecule to hin (dead until the
-    // node update) so the P rows can hold the waves' transposition slices, and restart macc from +0 (the pairs'
-    // aggregates are atomic, the receiver segments' first parts were stores)
-    // (not in the exact trace, whose block 1 runs dual tiles at one atom)
-    const bool pairs = kPairs && k == 0 && net.pairs && sparse_a < 0;
-    if (pairs) {
+    if (pairs && !pcopied) {
       for (int idx = tid; idx < (1 + NT) * MPW * 2 * M; idx += kNT) {   // primal rows, then the tangent rows
         const int w = idx / (MPW * 2 * M), m = (idx - w * MPW * 2 * M) / (2 * M), c = idx % (2 * M);
         s.hin[idx] = s.P[(w * RP + m * N) * s.ld_P + c];
